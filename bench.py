@@ -1,0 +1,308 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X-native local reduction (oneCCL src/comp hot path).
+
+Headline (BASELINE.json metric): GiB/s of device-resident fp32 sum-reduce of a
+1 GiB bucket.  One "step" = one ccl_comp_reduce-equivalent call through the C
+ABI (mi_reduce: inout += in over the whole bucket, inputs resident in HBM).
+
+  python bench.py [--gpus N --steps K --warmup W] [--config c2|c3-bf16|c3-fp16|c4|...]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Multi-GPU: the element range is sharded — every rank reduces
+its own 1 GiB bucket shard with no data-path collective ("scaling": "weak");
+torch.distributed is used only for the barrier and the max-over-ranks time.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+GiB = 1 << 30
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+# name -> (description, ccl dtype id, element size, op, n_inputs, bucket bytes, flags)
+CONFIGS = {
+    "c2": ("2-input fp32 sum-reduce, 1 GiB bucket, device-resident (BASELINE configs[1])", 9, 4, 0, 2, GiB, 0),
+    "c3-bf16": ("2-input bf16 sum, fp32 math + one RNE rounding, 256 MiB bucket (configs[2])", 11, 2, 0, 2,
+                256 << 20, 0x1 | 0x2),
+    "c3-fp16": ("2-input fp16 sum, fp32 math + one RNE rounding, 256 MiB bucket (configs[2])", 8, 2, 0, 2,
+                256 << 20, 0x1),
+    "c4": ("8-input fan-in fp32 sum (ring-chunk arrival pattern), 1 GiB bucket (configs[3])", 9, 4, 0, 8, GiB, 0),
+    "c4-bf16acc": ("8-input fan-in bf16 sum, fp32 accumulate, 1 GiB bucket", 11, 2, 0, 8, GiB, 0x4 | 0x2),
+    "c5-int32-max": ("2-input int32 max, 1 GiB bucket (configs[4])", 4, 4, 3, 2, GiB, 0),
+    "c5-int64-prod": ("2-input int64 prod, 1 GiB bucket (configs[4])", 6, 8, 1, 2, GiB, 0),
+}
+DTYPE_LABEL = {9: "f32", 11: "bf16 (f32 math)", 8: "f16 (f32 math)", 4: "int32", 6: "int64"}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: every GPU reduces its own full bucket; strong: one bucket split over the GPUs")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's work")
+    p.add_argument("--no-host-leg", action="store_true", help="skip the host-resident (PCIe) measurement")
+    return p.parse_args()
+
+
+def fill(t, seed):
+    """Synthetic inputs in [-1, 1) (fp) / small ints, generated on the device."""
+    import torch
+    g = torch.Generator(device=t.device)
+    g.manual_seed(seed)
+    if t.dtype.is_floating_point:
+        t.uniform_(-1.0, 1.0, generator=g)
+    else:
+        t.random_(-1000, 1000, generator=g)
+
+
+def torch_dtype(dt):
+    import torch
+    return {9: torch.float32, 11: torch.bfloat16, 8: torch.float16, 4: torch.int32, 6: torch.int64}[dt]
+
+
+def cpu_baseline(cfg, seconds):
+    """The oracle (CPU restatement of src/comp) timed on this host, bounded
+    sample: whole-bucket reduces repeated until ~`seconds` of CPU work."""
+    import numpy as np
+    import oracle
+    desc, dt, es, op, k, bucket, flags = cfg
+    n = bucket // es
+    rng = np.random.default_rng(0xC0FFEE)
+    npdt = oracle.NP_DTYPE[dt]
+    if dt in (9,):
+        ins = [rng.random(n, dtype=np.float32) * 2 - 1 for _ in range(k)]
+    elif dt in (4, 6):
+        ins = [rng.integers(-1000, 1000, n).astype(npdt) for _ in range(k)]
+    else:
+        f = rng.random(n, dtype=np.float32) * 2 - 1
+        ins = [oracle.f32_to_bf16(f, True) if dt == 11 else oracle.f32_to_fp16(f) for _ in range(k)]
+    acc = ins[0].copy()
+
+    def one(nthreads):
+        t0 = time.perf_counter()
+        for x in ins[1:]:
+            oracle.comp_reduce_mt(x, acc, dt, op, nthreads)  # chained 2-input calls, as the reference
+        return time.perf_counter() - t0
+
+    res = {}
+    for nthreads in (1, min(16, os.cpu_count() or 1)):
+        one(nthreads)  # first touch / warm
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 3 or (time.perf_counter() - t_start < seconds / 2 and len(times) < 200):
+            times.append(one(nthreads))
+        res[nthreads] = (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times))
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    (b1, m1, r1) = res[1]
+    nt = max(res)
+    (bn, mn, rn) = res[nt]
+    return {
+        "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"oracle/comp_oracle.c (CPU restatement of src/comp CCL_REDUCE loop, gcc -O3) on the same "
+                  f"{bucket // (1 << 20)} MiB bucket x {k}-input, best of {r1} reps (median {m1:.2f} GiB/s); "
+                  f"1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
+        "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": nt, "reps": rn,
+                         "note": "range split over threads, emulating CCL_WORKER_COUNT"},
+        "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from oneccl_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    cfg = CONFIGS[args.config]
+    desc, dt, es, op, k, bucket, flags = cfg
+    n_total = bucket // es
+    if args.scaling == "weak":
+        n = n_total
+    else:
+        import ctypes
+        lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+        _lib.check(_lib.mi().mi_shard_range(n_total, rank, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
+        n = hi.value - lo.value
+
+    m = _lib.mi()
+    tdt = torch_dtype(dt)
+    ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+    for j, t in enumerate(ins):
+        fill(t, 0xC0FFEE + 7919 * rank + j)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
+
+    def step():
+        if k == 2:
+            return m.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)  # inout += in
+        return m.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
+
+    # quick correctness probe on one element before timing (c2 only)
+    if args.config == "c2":
+        a0, b0 = ins[1][123].item(), ins[0][123].item()
+        _lib.check(step(), "mi_reduce")
+        torch.cuda.synchronize()
+        expect = torch.tensor(a0, dtype=torch.float32) + torch.tensor(b0, dtype=torch.float32)
+        assert ins[0][123].item() == expect.item(), "probe mismatch"
+
+    for _ in range(args.warmup):
+        _lib.check(step(), "mi_reduce")
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        rc = step()
+        ev[i][1].record(stream)
+        if rc:
+            _lib.check(rc, "mi_reduce")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_kern_ms = statistics.mean(kern_ms)
+
+    if world > 1:
+        t = torch.tensor([elapsed, avg_kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, avg_kern_ms_max = t.tolist()
+    else:
+        avg_kern_ms_max = avg_kern_ms
+
+    units_per_rank = n * es  # bucket bytes this rank reduced per step
+    total_bytes = units_per_rank * world if args.scaling == "weak" else n_total * es
+    value = total_bytes * args.steps / elapsed / GiB
+    traffic_per_launch = (k + 1) * n * es  # read k inputs, write 1 (algorithmic)
+    achieved = traffic_per_launch / (avg_kern_ms / 1e3) / 1e9
+
+    host_leg = None
+    if rank == 0 and world == 1 and not args.no_host_leg and k == 2:
+        host_leg = host_resident_leg(m, dt, es, op, flags, min(n, (256 << 20) // es))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, args.cpu_seconds)
+
+    traffic = pmc_traffic(args.config)
+    if rank == 0:
+        out = {
+            "metric": "GiB/s device-resident fp32 sum-reduce of 1 GiB bucket; 1/2/4/8 MI355X"
+            if args.config == "c2" else f"GiB/s device-resident {args.config} bucket reduce",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": DTYPE_LABEL.get(dt, str(dt)),
+            "data": "synthetic (uniform [-1,1) generated on device)",
+            "config": {"workload": desc, "bucket_bytes_per_gpu": units_per_rank, "inputs": k,
+                       "op": ["sum", "prod", "min", "max"][op], "dtype_id": dt, "flags": flags,
+                       "parallelism": f"element-range shard x{world}, no collective",
+                       "entry": "mi_reduce (include/mi_reduce.h) via ctypes, async on the torch stream"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                         "algorithmic_bytes_per_launch": traffic_per_launch,
+                         "avg_kernel_ms": round(avg_kern_ms, 5), "avg_kernel_ms_max_rank": round(avg_kern_ms_max, 5),
+                         "kernel_ms_min": round(min(kern_ms), 5),
+                         "timing": "hipEvent pair around each launch on the launch stream; mean over timed steps",
+                         "traffic_source": traffic.get("source") if traffic else None},
+            "cpu_baseline": cpu,
+        }
+        if host_leg:
+            out["host_resident"] = host_leg
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_resident_leg(m, dt, es, op, flags, n):
+    """The path as oneCCL runs it (host staging buffers in, host result out):
+    mi_reduce_sync with pinned and with pageable host buffers.  Reported
+    beside `value`, never as it (PCIe-inclusive rate)."""
+    import numpy as np
+    import torch
+    res = {}
+    nbytes = n * es
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            pa, pb = a.data_ptr(), b.data_ptr()
+        else:
+            a = np.zeros(nbytes, np.uint8)
+            b = np.zeros(nbytes, np.uint8)
+            pa, pb = a.ctypes.data, b.ctypes.data
+        m.mi_reduce_sync(pa, pb, n, dt, op, flags, -1)  # warm: staging buffers, page faults
+        times = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            rc = m.mi_reduce_sync(pa, pb, n, dt, op, flags, -1)
+            times.append(time.perf_counter() - t0)
+            if rc:
+                return {"error": m.mi_last_error().decode()}
+        res[kind] = round(nbytes / GiB / min(times), 3)
+    return {"unit": "GiB/s bucket incl. H2D of both operands and D2H of the result",
+            "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync"}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass
+    (profiles/*pmc*.json, produced by tools/pmc_traffic.py), if present."""
+    for p in sorted((ROOT / "profiles").glob("*pmc*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if config in d:
+            return {"bytes_per_launch": d[config]["hbm_bytes_per_launch"], "source": str(p.relative_to(ROOT))}
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+/*
+ * mi_ccl_comp.h — C view of the drop-in src/comp shim (libccl_comp_hip.so,
+ * built from oneccl_amd/csrc/comp.cpp in standalone mode).
+ *
+ * libccl_comp_hip.so exports oneCCL's own C++ entry points with identical
+ * mangled names (ccl_comp_reduce(ccl_sched*, ..., ccl::v1::reduction, ...),
+ * ccl_comp_batch_reduce, ccl_comp_copy, ccl_reduction_to_str,
+ * ccl_bf16_reduce, ccl_fp16_reduce — src/comp/comp.hpp:23-51,
+ * src/comp/bf16/bf16.hpp:26-38, src/comp/fp16/fp16.hpp:21-35).  The
+ * functions below are thin extern "C" wrappers over exactly those C++
+ * functions, so FFI callers (ctypes in this repo's tests, or a cgo/JNI
+ * binding) drive the same code path src/sched would.  Each returns the
+ * ccl::status value, or -1 if the C++ call threw (message:
+ * mi_ccl_last_error()).  dtype / op ids are ccl::datatype / ccl::reduction.
+ */
+#ifndef MI_CCL_COMP_H
+#define MI_CCL_COMP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ccl::reduction_fn with ccl::datatype passed as int
+ * (include/oneapi/ccl/types.hpp:122-124). */
+typedef void (*mi_ccl_reduction_fn)(const void* in_buf, size_t in_count, void* inout_buf,
+                                    size_t* out_count, int dtype, const void* context);
+
+/* ccl_comp_reduce(nullptr sched, ...), src/comp/comp.cpp:123-200 */
+int mi_ccl_comp_reduce(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
+                       int dtype, int op);
+/* ccl_comp_reduce with ccl::reduction::custom and a user callback,
+ * src/comp/comp.cpp:84-88 */
+int mi_ccl_comp_reduce_custom(const void* in_buf, size_t in_count, void* inout_buf,
+                              size_t* out_count, int dtype, mi_ccl_reduction_fn fn);
+/* ccl_comp_batch_reduce, src/comp/comp.cpp:202-249 */
+int mi_ccl_comp_batch_reduce(const void* in_buf, const size_t* offsets, size_t n_offsets,
+                             size_t in_count, void* inout_buf, size_t* out_count, int dtype,
+                             int op, int bf16_keep_precision_mode);
+/* ccl_comp_copy, src/comp/comp.cpp:60-74 */
+int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal);
+/* ccl_bf16_reduce, src/comp/bf16/bf16.cpp:87-110 (MPI user-op entry,
+ * src/atl/mpi/atl_mpi_ctx.cpp:87-92) */
+int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
+/* ccl_fp16_reduce, src/comp/fp16/fp16.cpp:41-53 */
+int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
+/* ccl_reduction_to_str, src/comp/comp.cpp:251-260 */
+const char* mi_ccl_reduction_to_str(int op);
+/* Re-read CCL_BF16 / CCL_FP16 / CCL_COMP_HIP_DEVICE (env.cpp:711-720). */
+int mi_ccl_env_reload(void);
+/* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
+int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
+const char* mi_ccl_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,183 @@
+/*
+ * mi_reduce.h — C ABI of the MI355X-native local element-wise reduction
+ * (libmi_reduce.so, built by hipcc for gfx950).
+ *
+ * This is the drop-in boundary that replaces the *body* of oneCCL's src/comp
+ * (reference snapshot 2024-12-20, v2021.14.0).  The C++ shim in
+ * oneccl_amd/csrc/comp.cpp keeps oneCCL's own signatures
+ * (ccl_comp_reduce / ccl_comp_batch_reduce / ccl_comp_copy /
+ * ccl_reduction_to_str / ccl_bf16_reduce / ccl_fp16_reduce) and calls down
+ * into the functions below, so src/sched, src/exec, src/coll, src/atl and the
+ * ccl:: API are untouched.
+ *
+ * Plain pointers and sizes only; no torch or HIP C++ types in signatures.
+ * `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *
+ * Return convention: 0 = success; MI_E_* (< 0) = argument / support errors;
+ * > 0 = the hipError_t that failed.  mi_last_error() returns a
+ * thread-local human-readable message for the last non-zero return.
+ * (The reference returns ccl::status::success always and CCL_FATALs on bad
+ * dtype/op, src/comp/comp.cpp:56,113; the C++ shim maps non-zero to
+ * CCL_THROW, see oneccl_amd/csrc/comp.cpp.)
+ */
+#ifndef MI_REDUCE_H
+#define MI_REDUCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- enumerations: numerically identical to the reference's ---------- */
+
+/* ccl::reduction — include/oneapi/ccl/types.hpp:41-47 */
+enum mi_op {
+    MI_OP_SUM = 0,
+    MI_OP_PROD = 1,
+    MI_OP_MIN = 2,
+    MI_OP_MAX = 3,
+    MI_OP_CUSTOM = 4 /* never accepted by the device entry points */
+};
+
+/* ccl::datatype — include/oneapi/ccl/types.hpp:52-69 */
+enum mi_dtype {
+    MI_INT8 = 0,
+    MI_UINT8 = 1,
+    MI_INT16 = 2,
+    MI_UINT16 = 3,
+    MI_INT32 = 4,
+    MI_UINT32 = 5,
+    MI_INT64 = 6,
+    MI_UINT64 = 7,
+    MI_FLOAT16 = 8,
+    MI_FLOAT32 = 9,
+    MI_FLOAT64 = 10,
+    MI_BFLOAT16 = 11
+};
+
+/* ---- semantic variant flags ------------------------------------------- *
+ * The reference's CPU reduce has several bit-level behaviours selected by
+ * CPUID / CCL_BF16 / CCL_FP16.  The device kernels implement
+ * every one of them; the caller picks with these flags.                    */
+
+/* min/max return `inout` when the operands are unordered (NaN) or equal
+ * (+0/-0): _mm512_min_ps(in, inout) semantics of the AVX-512 bf16/fp16
+ * paths (src/comp/bf16/bf16_intrisics.cpp:28-34,
+ * src/comp/fp16/fp16_intrisics.hpp:72-77).  Clear = std::min(in, inout)
+ * semantics of CCL_REDUCE and the scalar bf16 path (returns `in`),
+ * src/comp/comp.cpp:45-53, src/comp/bf16/bf16.cpp:42-48.                  */
+#define MI_F_MINMAX_INOUT_FIRST 0x1u
+/* fp32 -> bf16 by round-to-nearest-even with VCVTNEPS2BF16 semantics
+ * (denormal fp32 -> signed zero, NaN -> quiet NaN): avx512bf impl,
+ * src/comp/bf16/bf16_intrisics.hpp:72-76.  Clear = truncation (scalar and
+ * avx512f impls, bf16.cpp:50-54, bf16_intrisics.hpp:67-70).                */
+#define MI_F_BF16_RNE 0x2u
+/* Low-precision (bf16/fp16) fan-in accumulates in fp32 and rounds once at
+ * the end: ccl_comp_batch_reduce(..., bf16_keep_precision_mode=1, ...),
+ * src/comp/comp.cpp:214-234.  Clear = round to storage after every
+ * pairwise step (chained ccl_comp_reduce, comp.cpp:236-245).               */
+#define MI_F_ACC_FP32 0x4u
+/* With MI_F_ACC_FP32|MI_F_BF16_RNE: the last (count % 16) elements of the
+ * final fp32 -> bf16 conversion are truncated, as the scalar tail loop of
+ * ccl_convert_fp32_to_bf16_arrays does (src/comp/bf16/bf16.cpp:132-143).   */
+#define MI_F_BF16_TAIL_TRUNC16 0x8u
+
+/* Error codes (< 0). */
+#define MI_E_INVALID (-1)      /* bad dtype / op / k / NULL pointer      */
+#define MI_E_UNSUPPORTED (-2)  /* combination not implemented            */
+#define MI_E_NO_DEVICE (-3)    /* no HIP device visible                   */
+
+#define MI_MAX_INPUTS 16 /* the reference's monolithic fan-in covers 16 ranks
+                            (src/kernels/kernels.cl:268)                   */
+
+/* ---- device-resident entry points (asynchronous on `stream`) ---------- */
+
+/* inout[i] = op(in[i], inout[i]) for i < count.  Device pointers.
+ * Replaces the arithmetic of ccl_comp_reduce_regular, src/comp/comp.cpp:76-121
+ * (CCL_REDUCE :31-58; ccl_bf16_reduce bf16/bf16.cpp:87-110; ccl_fp16_reduce
+ * fp16/fp16.cpp:41-53) and the device kernel reduce_local_inplace_kernel_*,
+ * src/kernels/kernels.cl:236-246.                                           */
+int mi_reduce(const void* in, void* inout, size_t count, int dtype, int op,
+              unsigned flags, void* stream);
+
+/* out[i] = op(in1[i], in2[i]) with in1 in the `in` role and in2 in the
+ * `inout` role.  Replaces reduce_local_outofplace_kernel_*,
+ * src/kernels/kernels.cl:219-234.                                           */
+int mi_reduce_out(const void* in1, const void* in2, void* out, size_t count,
+                  int dtype, int op, unsigned flags, void* stream);
+
+/* K-input fan-in, 2 <= k <= MI_MAX_INPUTS: acc = inputs[0];
+ * acc = op(inputs[j], acc) for j = 1..k-1 (left fold, `inputs[j]` in the
+ * `in` role); out = acc.  `out` may alias inputs[0].  Replaces
+ * ccl_comp_batch_reduce, src/comp/comp.cpp:202-249, and the monolithic
+ * fan-in kernels reduce_monolithic_kernel_<N>_*, src/kernels/kernels.cl:269-421. */
+int mi_reduce_multi(const void* const* inputs, int k, void* out, size_t count,
+                    int dtype, int op, unsigned flags, void* stream);
+
+/* ---- synchronous, pointer-kind-agnostic entry (what src/comp calls) --- *
+ * Same math as mi_reduce, but `in`/`inout` may each be device memory,
+ * pinned host memory or pageable host memory; returns only when the result
+ * is in `inout` (the entries mark themselves complete right after the call:
+ * src/sched/entry/reduce_local_entry.cpp:113, recv_reduce_entry.hpp:133).
+ * Host operands are staged through the GPU in pipelined chunks (H2D, kernel,
+ * D2H on a per-thread stream).  `device` < 0 = the calling thread's current
+ * HIP device.  Thread-safe: each calling thread has its own stream and
+ * scratch (threading contract of src/exec/thread/worker.cpp:310-379).     */
+int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype,
+                   int op, unsigned flags, int device);
+
+/* Synchronous K-input fan-in with host-or-device operands (staged like
+ * mi_reduce_sync).  Used by ccl_comp_batch_reduce.                       */
+int mi_reduce_multi_sync(const void* const* inputs, int k, void* out,
+                         size_t count, int dtype, int op, unsigned flags,
+                         int device);
+
+/* Byte copy, synchronous, any pointer kinds.  Replaces the body of
+ * ccl_comp_copy, src/comp/comp.cpp:60-74 (nontemporal flag honoured on the
+ * device path by non-temporal stores).                                     */
+int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal,
+                 int device);
+
+/* Asynchronous device-to-device copy kernel (non-temporal stores if asked). */
+int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal,
+            void* stream);
+
+/* ---- element-range sharding for 1..8 GPUs ------------- *
+ * Contiguous [begin,end) of shard `rank` of `world`, boundaries rounded to
+ * `align` elements (0 -> 256).  No data moves: each GPU reduces its shard of
+ * every input independently; no collective is involved.                  */
+int mi_shard_range(size_t count, int rank, int world, size_t align,
+                   size_t* begin, size_t* end);
+
+/* ---- pointer classification ------------------------------------------- */
+/* 0 = device (or managed) memory of HIP device *device; 1 = pinned host
+ * memory; 2 = pageable host memory.  What ccl_comp_reduce's SYCL branch asks
+ * sycl::get_pointer_type for (src/comp/comp.cpp:145-147).                 */
+int mi_pointer_kind(const void* ptr, int* device);
+
+/* ---- introspection ---------------------------------------------------- */
+
+/* ccl_reduction_to_str, src/comp/comp.cpp:251-260. */
+const char* mi_reduction_to_str(int op);
+/* Size in bytes of a datatype id (0 if unknown);
+ * src/common/datatype/datatype.cpp predefined table.                      */
+size_t mi_dtype_size(int dtype);
+/* Thread-local message for the last non-zero return on this thread. */
+const char* mi_last_error(void);
+/* ABI version: major*10000 + minor*100 + patch. */
+int mi_version(void);
+/* Number of HIP devices (0 when none).  Never initialises a context.      */
+int mi_device_count(void);
+/* Launch geometry the vector kernels use: threads per block, 16-byte
+ * vectors per lane per tile, and the grid cap (0 = one tile per block).   */
+int mi_get_launch_config(int* block, int* unroll, int* max_blocks);
+/* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS). */
+int mi_set_max_blocks(int max_blocks);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI_REDUCE_H */

@@ -1,0 +1,93 @@
+"""In-tree build of the native libraries (no JIT cache: the .so files live in
+oneccl_amd/lib/ and travel with the repo snapshot to the GPU box).
+
+  libmi_reduce.so     hipcc --offload-arch=gfx950: kernels + C ABI
+                      (include/mi_reduce.h)
+  libccl_comp_hip.so  g++: the drop-in src/comp shim (oneCCL's C++ entry
+                      points, include/mi_ccl_comp.h), linked to libmi_reduce.so
+  tools/reduce_sweep  hipcc: launch-geometry / load-policy sweep (bench tool)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "lib"
+ARCH = os.environ.get("MI_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X build needs ROCm's hipcc")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_mi_reduce(force: bool = False) -> Path:
+    out = LIB / "libmi_reduce.so"
+    deps = [CSRC / "mi_reduce.hip", CSRC / "reduce_kernels.hpp", ROOT / "include" / "mi_reduce.h"]
+    if force or _stale(out, deps):
+        LIB.mkdir(exist_ok=True)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+              "-o", str(out), str(CSRC / "mi_reduce.hip")])
+    return out
+
+
+def build_shim(force: bool = False) -> Path:
+    out = LIB / "libccl_comp_hip.so"
+    deps = [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_reduce.h",
+            ROOT / "include" / "mi_ccl_comp.h", LIB / "libmi_reduce.so"]
+    if force or _stale(out, deps):
+        cxx = os.environ.get("CXX", "g++")
+        _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
+              "-o", str(out), str(CSRC / "comp.cpp"),
+              f"-L{LIB}", "-lmi_reduce", "-Wl,-rpath,$ORIGIN"])
+    return out
+
+
+def build_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "reduce_sweep"
+    src = ROOT / "tools" / "reduce_sweep.hip"
+    deps = [src, CSRC / "reduce_kernels.hpp"]
+    if src.exists() and (force or _stale(out, deps)):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall",
+              "-o", str(out), str(src)])
+    return out
+
+
+def build_oracle(force: bool = False) -> Path:
+    """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile)."""
+    odir = ROOT / "oracle"
+    if force:
+        _run(["make", "-C", str(odir), "clean"])
+    _run(["make", "-C", str(odir), "-j4"])
+    return odir / "lib" / "libcomp_oracle.so"
+
+
+def build_all(force: bool = False) -> None:
+    build_mi_reduce(force)
+    build_shim(force)
+    build_sweep(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,422 @@
+// comp.cpp — drop-in replacement for oneCCL's src/comp/*.cpp, backed by the
+// MI355X HIP kernels of libmi_reduce.so (include/mi_reduce.h).
+//
+// Keeps the reference's signatures and semantics:
+//   ccl_comp_copy           src/comp/comp.cpp:60-74
+//   ccl_comp_reduce         src/comp/comp.cpp:123-200  (+ _regular :76-121)
+//   ccl_comp_batch_reduce   src/comp/comp.cpp:202-249
+//   ccl_reduction_to_str    src/comp/comp.cpp:251-260
+//   ccl_bf16_reduce         src/comp/bf16/bf16.cpp:87-110
+//   ccl_fp16_reduce         src/comp/fp16/fp16.cpp:41-53
+//   bf16_impl_names / fp16_impl_names / fp16_env_impl_names (bf16.cpp:29-33, fp16.cpp:29-41)
+// Which bit-level behaviour the reference would show (bf16 truncation vs
+// RNE, min/max operand order) is taken from the same place the reference
+// takes it: the bf16/fp16 impl type chosen from CPUID and CCL_BF16/CCL_FP16
+// (src/common/env/env.cpp:711-720).
+//
+// Build modes:
+//   -DMI_ONECCL_TREE : compiled inside oneCCL's src/ (see INTEGRATION.md),
+//                      uses the real headers, ccl::global_data::env() and
+//                      CCL_THROW.
+//   default          : standalone libccl_comp_hip.so for this repo's tests and
+//                      bench (ccl_mirror.hpp; same mangled symbols).
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mi_reduce.h"
+
+#ifdef MI_ONECCL_TREE
+#include "common/global/global.hpp"
+#include "common/log/log.hpp"
+#include "comp/bf16/bf16.hpp"
+#include "comp/comp.hpp"
+#include "comp/fp16/fp16.hpp"
+#define MI_CCL_THROW(msg) CCL_THROW(msg)
+static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
+static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
+static int mi_comp_device() { return -1; }
+#else
+#include "../../include/mi_ccl_comp.h"
+#include "ccl_mirror.hpp"
+#define MI_CCL_THROW(msg) throw ccl::exception(msg)
+#endif
+
+// bf16.cpp:29-33, fp16.cpp:29-41 — referenced by env.cpp:711-720, 1101-1102
+std::map<ccl_bf16_impl_type, std::string> bf16_impl_names = {
+    std::make_pair(ccl_bf16_scalar, "scalar"), std::make_pair(ccl_bf16_avx512f, "avx512f"),
+    std::make_pair(ccl_bf16_avx512bf, "avx512bf")};
+
+std::map<ccl_fp16_impl_type, std::string> fp16_impl_names = {
+    std::make_pair(ccl_fp16_no_compiler_support, "no_compiler_support"),
+    std::make_pair(ccl_fp16_no_hardware_support, "no_hardware_support"),
+    std::make_pair(ccl_fp16_f16c, "f16c"), std::make_pair(ccl_fp16_avx512f, "avx512f"),
+    std::make_pair(ccl_fp16_avx512fp16, "avx512fp16")};
+
+std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
+    std::make_pair(ccl_fp16_f16c, "f16c"), std::make_pair(ccl_fp16_avx512f, "avx512f"),
+    std::make_pair(ccl_fp16_avx512fp16, "avx512fp16")};
+
+#ifndef MI_ONECCL_TREE
+// ---------------------------------------------------------------------------
+// standalone environment: the reference's CPUID detection
+// (src/comp/bf16/bf16_utils.hpp:30-68, src/comp/fp16/fp16_utils.hpp:37-88)
+// then the CCL_BF16 / CCL_FP16 override (src/common/env/env.cpp:711-720)
+// ---------------------------------------------------------------------------
+namespace {
+
+struct MiEnv {
+    ccl_bf16_impl_type bf16 = ccl_bf16_scalar;
+    ccl_fp16_impl_type fp16 = ccl_fp16_no_compiler_support;
+    int device = -1;  // CCL_COMP_HIP_DEVICE
+};
+
+std::mutex g_env_mu;
+MiEnv g_env;
+bool g_env_ready = false;
+
+void cpuid(uint32_t leaf, uint32_t sub, uint32_t r[4]) {
+#if defined(__x86_64__) || defined(__i386__)
+    __asm__ __volatile__("cpuid" : "=a"(r[0]), "=b"(r[1]), "=c"(r[2]), "=d"(r[3]) : "a"(leaf), "c"(sub));
+#else
+    r[0] = r[1] = r[2] = r[3] = 0;
+#endif
+}
+
+std::set<ccl_bf16_impl_type> bf16_impl_types() {
+    std::set<ccl_bf16_impl_type> s{ccl_bf16_scalar};
+    uint32_t r[4];
+    cpuid(7, 0, r);
+    const bool f = ((r[1] >> 16) & 1) && ((r[1] >> 30) & 1) && ((r[1] >> 31) & 1);
+    cpuid(7, 1, r);
+    const bool bf = (r[0] >> 5) & 1;
+    if (f) s.insert(ccl_bf16_avx512f);
+    if (bf) s.insert(ccl_bf16_avx512bf);
+    return s;
+}
+
+std::set<ccl_fp16_impl_type> fp16_impl_types() {
+    std::set<ccl_fp16_impl_type> s;
+    uint32_t r[4];
+    cpuid(1, 0, r);
+    const bool f16c = (r[2] >> 29) & 1;
+    cpuid(7, 0, r);
+    const bool f = ((r[1] >> 16) & 1) && ((r[1] >> 30) & 1) && ((r[1] >> 31) & 1);
+    const bool fp16 = ((r[1] >> 30) & 1) && ((r[3] >> 23) & 1);
+    if (fp16) s.insert(ccl_fp16_avx512fp16);
+    if (f) s.insert(ccl_fp16_avx512f);
+    if (f16c) s.insert(ccl_fp16_f16c);
+    if (!fp16 && !f && !f16c) s.insert(ccl_fp16_no_hardware_support);
+    return s;
+}
+
+void parse_env_locked() {
+    MiEnv e;
+    e.bf16 = *bf16_impl_types().rbegin();
+    if (const char* v = getenv("CCL_BF16")) {
+        bool found = false;
+        for (auto& kv : bf16_impl_names)
+            if (kv.second == v) {
+                e.bf16 = kv.first;
+                found = true;
+            }
+        if (!found) MI_CCL_THROW(std::string("unexpected CCL_BF16 value: ") + v);
+    }
+    auto fp16_types = fp16_impl_types();
+    e.fp16 = *fp16_types.rbegin();
+    if (const char* v = getenv("CCL_FP16")) {
+        bool found = false;
+        for (auto& kv : fp16_env_impl_names)
+            if (kv.second == v) {
+                e.fp16 = kv.first;
+                found = true;
+            }
+        if (!found) MI_CCL_THROW(std::string("unexpected CCL_FP16 value: ") + v);
+    }
+    if (fp16_types.find(e.fp16) == fp16_types.end())
+        MI_CCL_THROW("unsupported FP16 impl type: " + fp16_impl_names[e.fp16]);
+    if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) e.device = atoi(v);
+    g_env = e;
+    g_env_ready = true;
+}
+
+const MiEnv& env() {
+    std::lock_guard<std::mutex> g(g_env_mu);
+    if (!g_env_ready) parse_env_locked();
+    return g_env;
+}
+
+}  // namespace
+
+static ccl_bf16_impl_type mi_bf16_impl() { return env().bf16; }
+static ccl_fp16_impl_type mi_fp16_impl() { return env().fp16; }
+static int mi_comp_device() { return env().device; }
+#endif  // !MI_ONECCL_TREE
+
+// ---------------------------------------------------------------------------
+// semantics selection
+// ---------------------------------------------------------------------------
+namespace {
+
+unsigned bf16_flags(ccl_bf16_impl_type impl) {
+    switch (impl) {
+        case ccl_bf16_scalar: return 0u;  // std::min/max, truncate (bf16.cpp:63-85)
+        case ccl_bf16_avx512f: return MI_F_MINMAX_INOUT_FIRST;  // MINPS order, truncate
+        case ccl_bf16_avx512bf: return MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE;
+    }
+    return 0u;
+}
+
+// fp16: f16c / avx512f / avx512fp16 all compute in (or exactly as) fp32 with
+// MINPS order and RNE (fp16_intrisics.hpp:204-248); any other impl computes
+// nothing (it falls through every branch) — reproduced by returning false.
+bool fp16_flags(ccl_fp16_impl_type impl, unsigned* f) {
+    *f = MI_F_MINMAX_INOUT_FIRST;
+    return impl == ccl_fp16_f16c || impl == ccl_fp16_avx512f || impl == ccl_fp16_avx512fp16;
+}
+
+void check(int rc, const char* where) {
+    if (rc != 0) MI_CCL_THROW(std::string(where) + " failed: " + mi_last_error());
+}
+
+bool is_device_ptr(const void* p) {
+    int dev = -1;
+    return mi_pointer_kind(p, &dev) == 0;
+}
+
+// reference behaviour for a user callback (comp.cpp:84-88); device operands
+// are staged through host memory, as the reference's SYCL branch does
+// (comp.cpp:136-195)
+void run_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
+                const ccl_datatype& dtype, ccl::reduction_fn fn, const ccl::fn_context* context) {
+    if (!fn) MI_CCL_THROW("custom reduction requires user callback");
+    const bool din = is_device_ptr(in_buf), dio = is_device_ptr(inout_buf);
+    if (!din && !dio) {
+        fn(in_buf, in_count, inout_buf, out_count, dtype.idx(), context);
+        return;
+    }
+    const size_t bytes = in_count * dtype.size();
+    std::vector<char> hin, hio;
+    const void* in_h = in_buf;
+    void* io_h = inout_buf;
+    if (din) {
+        hin.resize(bytes);
+        check(mi_copy_sync(in_buf, hin.data(), bytes, 0, -1), "mi_copy_sync");
+        in_h = hin.data();
+    }
+    if (dio) {
+        hio.resize(bytes);
+        check(mi_copy_sync(inout_buf, hio.data(), bytes, 0, -1), "mi_copy_sync");
+        io_h = hio.data();
+    }
+    fn(in_h, in_count, io_h, out_count, dtype.idx(), context);
+    if (dio) check(mi_copy_sync(hio.data(), inout_buf, bytes, 0, -1), "mi_copy_sync");
+}
+
+int dtype_id(const ccl_datatype& dt) { return static_cast<int>(dt.idx()); }
+
+}  // namespace
+
+// ===========================================================================
+// oneCCL entry points
+// ===========================================================================
+
+ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool use_nontemporal) {
+    if (bytes == 0) return ccl::status::success;
+    if (!in_buf) MI_CCL_THROW("in_buf is null");
+    if (!out_buf) MI_CCL_THROW("out_buf is null");
+    check(mi_copy_sync(in_buf, out_buf, bytes, use_nontemporal ? 1 : 0, mi_comp_device()), "mi_copy_sync");
+    return ccl::status::success;
+}
+
+void ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
+    if (out_cnt != nullptr) *out_cnt = in_cnt;
+    if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
+    check(mi_reduce_sync(in_buf, inout_buf, in_cnt, MI_BFLOAT16, static_cast<int>(op),
+                         bf16_flags(mi_bf16_impl()), mi_comp_device()),
+          "mi_reduce_sync(bf16)");
+}
+
+void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
+    if (out_cnt != nullptr) *out_cnt = in_cnt;
+    if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
+    unsigned f = 0;
+    if (!fp16_flags(mi_fp16_impl(), &f)) return;
+    check(mi_reduce_sync(in_buf, inout_buf, in_cnt, MI_FLOAT16, static_cast<int>(op), f, mi_comp_device()),
+          "mi_reduce_sync(fp16)");
+}
+
+// ccl_comp_reduce_regular, comp.cpp:76-121
+static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
+                                       const ccl_datatype& dtype, ccl::reduction reduction,
+                                       ccl::reduction_fn reduction_fn, const ccl::fn_context* context) {
+    if (reduction == ccl::reduction::custom) {
+        run_custom(in_buf, in_count, inout_buf, out_count, dtype, reduction_fn, context);
+        return ccl::status::success;
+    }
+    const int dt = dtype_id(dtype);
+    if (mi_dtype_size(dt) == 0) MI_CCL_THROW("unexpected value " + std::to_string(dt));
+    if (dt == MI_BFLOAT16) {
+        ccl_bf16_reduce(in_buf, in_count, inout_buf, out_count, reduction);
+    } else if (dt == MI_FLOAT16) {
+        ccl_fp16_reduce(in_buf, in_count, inout_buf, out_count, reduction);
+    } else {
+        // CCL_REDUCE: std::min/std::max operand order, no out_count write
+        check(mi_reduce_sync(in_buf, inout_buf, in_count, dt, static_cast<int>(reduction), 0u, mi_comp_device()),
+              "mi_reduce_sync");
+    }
+    return ccl::status::success;
+}
+
+ccl::status ccl_comp_reduce(ccl_sched* /*sched*/, const void* in_buf, size_t in_count, void* inout_buf,
+                            size_t* out_count, const ccl_datatype& dtype, ccl::reduction reduction,
+                            ccl::reduction_fn reduction_fn, const ccl::fn_context* context) {
+    if (!in_count) return ccl::status::success;
+    return comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
+}
+
+ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
+                                  void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
+                                  ccl::reduction reduction, ccl::reduction_fn reduction_fn,
+                                  const ccl::fn_context* context, int bf16_keep_precision_mode, float* /*tmp*/,
+                                  float* /*acc*/) {
+    // The fp32 scratch `tmp`/`acc` of the reference (comp.cpp:210-234) is not
+    // needed: the kernel keeps the fp32 accumulator in registers.
+    const size_t es = dtype.size();
+    if (bf16_keep_precision_mode) {
+        // keep-precision: buffers read as bf16 whatever dtype says; inputs
+        // strided by dtype.size() (comp.cpp:214-234)
+        if (reduction == ccl::reduction::custom)
+            MI_CCL_THROW("custom reduction is not supported in bf16 keep-precision mode");
+        const size_t k = std::max<size_t>(offsets.size(), 1);
+        if (k > MI_MAX_INPUTS) MI_CCL_THROW("keep-precision fan-in supports at most 16 inputs");
+        if (in_count == 0) return ccl::status::success;
+        std::vector<const void*> ins(k);
+        ins[0] = inout_buf;
+        for (size_t i = 1; i < k; i++) ins[i] = static_cast<const char*>(in_buf) + es * offsets[i];
+        // acc uses CCL_REDUCE(float) order (std::min/max); final conversion
+        // per impl: avx512bf RNE on (count/16)*16 elements + truncated tail,
+        // avx512f / scalar truncate all (bf16.cpp:113-143)
+        unsigned f = MI_F_ACC_FP32;
+        if (mi_bf16_impl() == ccl_bf16_avx512bf) f |= MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16;
+        check(mi_reduce_multi_sync(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16,
+                                   static_cast<int>(reduction), f, mi_comp_device()),
+              "mi_reduce_multi_sync");
+        return ccl::status::success;
+    }
+    if (offsets.size() <= 1 || in_count == 0) return ccl::status::success;
+    if (reduction == ccl::reduction::custom) {
+        for (size_t i = 1; i < offsets.size(); i++)
+            comp_reduce_regular(static_cast<const char*>(in_buf) + es * offsets[i], in_count, inout_buf, out_count,
+                                dtype, reduction, reduction_fn, context);
+        return ccl::status::success;
+    }
+    // storage-precision left fold == the reference's chained reduces
+    const int dt = dtype_id(dtype);
+    unsigned f = 0;
+    if (dt == MI_BFLOAT16) {
+        f = bf16_flags(mi_bf16_impl());
+    } else if (dt == MI_FLOAT16) {
+        if (!fp16_flags(mi_fp16_impl(), &f)) return ccl::status::success;
+    }
+    if ((dt == MI_BFLOAT16 || dt == MI_FLOAT16) && out_count) *out_count = in_count;
+    size_t next = 1;
+    while (next < offsets.size()) {
+        const void* ins[MI_MAX_INPUTS];
+        int k = 0;
+        ins[k++] = inout_buf;
+        while (next < offsets.size() && k < MI_MAX_INPUTS)
+            ins[k++] = static_cast<const char*>(in_buf) + es * offsets[next++];
+        check(mi_reduce_multi_sync(ins, k, inout_buf, in_count, dt, static_cast<int>(reduction), f, mi_comp_device()),
+              "mi_reduce_multi_sync");
+    }
+    return ccl::status::success;
+}
+
+const char* ccl_reduction_to_str(ccl::reduction type) { return mi_reduction_to_str(static_cast<int>(type)); }
+
+#ifndef MI_ONECCL_TREE
+// ===========================================================================
+// C view of the shim (include/mi_ccl_comp.h) — lets tests and ctypes/FFI
+// callers drive exactly the code path src/sched would.
+// ===========================================================================
+namespace {
+thread_local std::string t_shim_err;
+ccl_datatype mk_dtype(int dt) { return ccl_datatype(static_cast<ccl::datatype>(dt), mi_dtype_size(dt)); }
+}  // namespace
+
+#define MI_SHIM_GUARD(body)                 \
+    try {                                   \
+        body;                               \
+    } catch (const std::exception& e) {     \
+        t_shim_err = e.what();              \
+        return -1;                          \
+    }
+
+extern "C" {
+
+int mi_ccl_comp_reduce(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype, int op) {
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce(nullptr, in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                              static_cast<ccl::reduction>(op), nullptr, nullptr));
+}
+
+int mi_ccl_comp_reduce_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype,
+                              mi_ccl_reduction_fn fn) {
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce(nullptr, in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                              ccl::reduction::custom, reinterpret_cast<ccl::reduction_fn>(fn),
+                                              nullptr));
+}
+
+int mi_ccl_comp_batch_reduce(const void* in_buf, const size_t* offsets, size_t n_offsets, size_t in_count,
+                             void* inout_buf, size_t* out_count, int dtype, int op, int bf16_keep_precision_mode) {
+    MI_SHIM_GUARD({
+        std::vector<size_t> offs(offsets, offsets + n_offsets);
+        return (int)ccl_comp_batch_reduce(in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                          static_cast<ccl::reduction>(op), nullptr, nullptr,
+                                          bf16_keep_precision_mode, nullptr, nullptr);
+    });
+}
+
+int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal) {
+    MI_SHIM_GUARD(return (int)ccl_comp_copy(in_buf, out_buf, bytes, use_nontemporal != 0));
+}
+
+int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
+    MI_SHIM_GUARD({
+        ccl_bf16_reduce(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
+        return 0;
+    });
+}
+
+int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
+    MI_SHIM_GUARD({
+        ccl_fp16_reduce(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
+        return 0;
+    });
+}
+
+const char* mi_ccl_reduction_to_str(int op) { return ccl_reduction_to_str(static_cast<ccl::reduction>(op)); }
+
+int mi_ccl_env_reload(void) {
+    MI_SHIM_GUARD({
+        std::lock_guard<std::mutex> g(g_env_mu);
+        parse_env_locked();
+        return 0;
+    });
+}
+
+int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl) {
+    MI_SHIM_GUARD({
+        const MiEnv& e = env();
+        if (bf16_impl) *bf16_impl = (int)e.bf16;
+        if (fp16_impl) *fp16_impl = (int)e.fp16;
+        return 0;
+    });
+}
+
+const char* mi_ccl_last_error(void) { return t_shim_err.c_str(); }
+
+}  // extern "C"
+#endif  // !MI_ONECCL_TREE

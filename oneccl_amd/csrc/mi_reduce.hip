@@ -1,0 +1,548 @@
+// mi_reduce.hip — libmi_reduce.so: the C ABI of include/mi_reduce.h.
+//
+// Host half of the MI355X-native local reduction: variant canonicalisation,
+// kernel selection, launch geometry, per-thread streams and the
+// host-operand staging pipeline.  Kernels: reduce_kernels.hpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mi_reduce.h"
+#include "reduce_kernels.hpp"
+
+using namespace mi;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what) {
+    g_last_error = what;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return (int)e;
+}
+#define MI_HIP(call)                                   \
+    do {                                               \
+        hipError_t e_ = (call);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// launch configuration
+// ---------------------------------------------------------------------------
+constexpr int kUnroll = 4;  // 16-byte vectors per lane per input per tile
+constexpr int kMem = 2;     // plain loads, non-temporal stores
+
+std::atomic<int> g_max_blocks{-1};  // -1 = not yet read from env; 0 = no cap
+
+int max_blocks() {
+    int v = g_max_blocks.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* s = getenv("MI_REDUCE_MAX_BLOCKS");
+        v = s ? std::max(0, atoi(s)) : 0;
+        g_max_blocks.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
+size_t dtype_size(int dt) {
+    switch (dt) {
+        case MI_INT8: case MI_UINT8: return 1;
+        case MI_INT16: case MI_UINT16: case MI_FLOAT16: case MI_BFLOAT16: return 2;
+        case MI_INT32: case MI_UINT32: case MI_FLOAT32: return 4;
+        case MI_INT64: case MI_UINT64: case MI_FLOAT64: return 8;
+        default: return 0;
+    }
+}
+
+// Keep only the variant bits that change results for (dtype, op, k).
+unsigned canon_flags(int dt, int op, unsigned f, int k) {
+    const bool mm = (op == MI_OP_MIN || op == MI_OP_MAX);
+    switch (dt) {
+        case MI_FLOAT32:
+        case MI_FLOAT64: return mm ? (f & V_INOUT_FIRST) : 0u;
+        case MI_FLOAT16: {
+            unsigned v = (mm ? (f & V_INOUT_FIRST) : 0u) | (f & V_ACC_FP32);
+            if (k <= 2) v &= ~V_ACC_FP32;  // one step: same single rounding
+            return v;
+        }
+        case MI_BFLOAT16: {
+            unsigned v = (mm ? (f & V_INOUT_FIRST) : 0u) | (f & (V_BF16_RNE | V_ACC_FP32 | V_TAIL_TRUNC));
+            if (!((v & V_ACC_FP32) && (v & V_BF16_RNE))) v &= ~V_TAIL_TRUNC;
+            if (k == 2 && !(v & V_TAIL_TRUNC)) v &= ~V_ACC_FP32;
+            return v;
+        }
+        default: return 0u;  // integers: no variants
+    }
+}
+
+// ---------------------------------------------------------------------------
+// kernel table
+// ---------------------------------------------------------------------------
+typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
+
+template <typename Tag, int OP, unsigned V, int KT>
+hipError_t launch_one(dim3 grid, hipStream_t s, const KArgs& a) {
+    hipLaunchKernelGGL((reduce_kernel<Tag, OP, V, KT, kUnroll, kMem>), grid, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename Tag, int OP, unsigned V>
+constexpr bool valid_v() {
+    constexpr bool mm = (OP == OP_MIN || OP == OP_MAX);
+    if constexpr (!Tr<Tag>::fp) return V == 0;
+    if constexpr (!Tr<Tag>::lp) return V == 0 || (mm && V == V_INOUT_FIRST);
+    if ((V & V_INOUT_FIRST) && !mm) return false;
+    if constexpr (std::is_same<Tag, fp16_tag>::value) return (V & (V_BF16_RNE | V_TAIL_TRUNC)) == 0;
+    if ((V & V_TAIL_TRUNC) && !((V & V_ACC_FP32) && (V & V_BF16_RNE))) return false;
+    return true;
+}
+
+template <typename Tag, int OP, unsigned V>
+LaunchFn entry(bool k2) {
+    if constexpr (valid_v<Tag, OP, V>())
+        return k2 ? &launch_one<Tag, OP, V, 2> : &launch_one<Tag, OP, V, 0>;
+    else
+        return nullptr;
+}
+
+template <typename Tag, int OP>
+LaunchFn pick_v(unsigned v, bool k2) {
+    switch (v) {
+#define MI_V(n) case n: return entry<Tag, OP, n##u>(k2);
+        MI_V(0) MI_V(1) MI_V(2) MI_V(3) MI_V(4) MI_V(5) MI_V(6) MI_V(7)
+        MI_V(8) MI_V(9) MI_V(10) MI_V(11) MI_V(12) MI_V(13) MI_V(14) MI_V(15)
+#undef MI_V
+        default: return nullptr;
+    }
+}
+
+template <typename Tag>
+LaunchFn pick_op(int op, unsigned v, bool k2) {
+    switch (op) {
+        case MI_OP_SUM: return pick_v<Tag, OP_SUM>(v, k2);
+        case MI_OP_PROD: return pick_v<Tag, OP_PROD>(v, k2);
+        case MI_OP_MIN: return pick_v<Tag, OP_MIN>(v, k2);
+        case MI_OP_MAX: return pick_v<Tag, OP_MAX>(v, k2);
+        default: return nullptr;
+    }
+}
+
+LaunchFn pick(int dt, int op, unsigned v, bool k2) {
+    switch (dt) {
+        case MI_INT8: return pick_op<int8_t>(op, v, k2);
+        case MI_UINT8: return pick_op<uint8_t>(op, v, k2);
+        case MI_INT16: return pick_op<int16_t>(op, v, k2);
+        case MI_UINT16: return pick_op<uint16_t>(op, v, k2);
+        case MI_INT32: return pick_op<int32_t>(op, v, k2);
+        case MI_UINT32: return pick_op<uint32_t>(op, v, k2);
+        case MI_INT64: return pick_op<int64_t>(op, v, k2);
+        case MI_UINT64: return pick_op<uint64_t>(op, v, k2);
+        case MI_FLOAT16: return pick_op<fp16_tag>(op, v, k2);
+        case MI_FLOAT32: return pick_op<float>(op, v, k2);
+        case MI_FLOAT64: return pick_op<double>(op, v, k2);
+        case MI_BFLOAT16: return pick_op<bf16_tag>(op, v, k2);
+        default: return nullptr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the asynchronous core: out = fold(inputs[0..k-1]) on device pointers
+// ---------------------------------------------------------------------------
+int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
+                  unsigned flags, hipStream_t stream) {
+    const size_t es = dtype_size(dt);
+    if (!es) return fail(MI_E_INVALID, "unknown datatype");
+    if (op < MI_OP_SUM || op > MI_OP_MAX) return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
+    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+    if (count == 0) return 0;
+    if (!out) return fail(MI_E_INVALID, "null output");
+    for (int i = 0; i < k; i++)
+        if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+
+    const unsigned v = canon_flags(dt, op, flags, k);
+    if (k == 1 && !(v & V_ACC_FP32)) {  // nothing to combine: result is inputs[0]
+        if (out != inputs[0]) MI_HIP(hipMemcpyAsync(out, inputs[0], count * es, hipMemcpyDeviceToDevice, stream));
+        return 0;
+    }
+    LaunchFn fn = pick(dt, op, v, k == 2);
+    if (!fn) return fail(MI_E_UNSUPPORTED, "no kernel for this dtype/op/variant");
+
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int i = 0; i < k; i++) a.in[i] = inputs[i];
+    a.out = out;
+    a.k = k;
+    a.count = count;
+    // VCVTNEPS2BF16 main part / scalar tail split of ccl_convert_fp32_to_bf16_arrays
+    a.trunc_from = (count / 16) * 16;
+
+    // common misalignment -> scalar head; different misalignments -> scalar loop
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(out) & 15u;
+    bool same = (mis % es) == 0;
+    for (int i = 0; i < k && same; i++) same = ((reinterpret_cast<uintptr_t>(inputs[i]) & 15u) == mis);
+    const size_t n_per_vec = 16 / es;
+    uint64_t blocks;
+    if (same) {
+        const size_t head = mis ? std::min<size_t>((16 - mis) / es, count) : 0;
+        const size_t body = count - head;
+        a.head = head;
+        a.nvec = body / n_per_vec;
+        a.tail = body - a.nvec * n_per_vec;
+        const uint64_t tile = (uint64_t)kBlock * kUnroll;
+        blocks = (a.nvec + tile - 1) / tile;
+        const int cap = max_blocks();
+        if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
+        if (blocks == 0) blocks = 1;
+    } else {
+        a.scalar_only = 1;
+        blocks = std::min<uint64_t>((count + kBlock - 1) / kBlock, 8192);
+    }
+    if (blocks > 0x7FFFFFFFull) blocks = 0x7FFFFFFFull;
+    hipError_t e = fn(dim3((unsigned)blocks), stream, a);
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// per-thread device context: stream + scratch for host-operand staging
+// ---------------------------------------------------------------------------
+constexpr size_t kChunkBytes = 32ull << 20;  // staging chunk per operand
+
+struct DevCtx {
+    int device = -1;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    std::vector<void*> dbuf[2];  // per pipeline slot: one device buffer per host operand
+    size_t dbuf_bytes = 0;
+
+    ~DevCtx() {
+        // Contexts die with their thread; device teardown at process exit may
+        // already have happened, so errors here are ignored.
+        for (int s = 0; s < 2; s++) {
+            for (void* p : dbuf[s]) (void)hipFree(p);
+            if (stream[s]) (void)hipStreamDestroy(stream[s]);
+        }
+    }
+};
+
+struct ThreadCtx {
+    std::vector<DevCtx*> devs;
+    ~ThreadCtx() {
+        for (DevCtx* d : devs) delete d;
+    }
+};
+thread_local ThreadCtx t_ctx;
+
+int get_ctx(int device, DevCtx** out) {
+    if (device < 0) MI_HIP(hipGetDevice(&device));
+    if ((size_t)device >= t_ctx.devs.size()) t_ctx.devs.resize(device + 1, nullptr);
+    DevCtx*& d = t_ctx.devs[device];
+    if (!d) {
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        MI_HIP(hipSetDevice(device));
+        d = new DevCtx();
+        d->device = device;
+        for (int s = 0; s < 2; s++) MI_HIP(hipStreamCreateWithFlags(&d->stream[s], hipStreamNonBlocking));
+        MI_HIP(hipSetDevice(prev));
+    }
+    *out = d;
+    return 0;
+}
+
+int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
+    if (d->dbuf[0].size() >= nbuf && d->dbuf_bytes >= bytes) return 0;
+    for (int s = 0; s < 2; s++) {
+        for (void* p : d->dbuf[s]) MI_HIP(hipFree(p));
+        d->dbuf[s].clear();
+    }
+    d->dbuf_bytes = std::max(bytes, d->dbuf_bytes);
+    nbuf = std::max(nbuf, d->dbuf[0].size());
+    for (int s = 0; s < 2; s++) {
+        d->dbuf[s].resize(nbuf, nullptr);
+        for (size_t i = 0; i < nbuf; i++) MI_HIP(hipMalloc(&d->dbuf[s][i], d->dbuf_bytes));
+    }
+    return 0;
+}
+
+enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
+
+PtrKind classify(const void* p, int* dev) {
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof(at));
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // clear the sticky "invalid value" for unregistered memory
+        return PK_PAGEABLE;
+    }
+    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) {
+        *dev = at.device;
+        return PK_DEVICE;
+    }
+    if (at.type == hipMemoryTypeHost) return PK_PINNED;
+    return PK_PAGEABLE;
+}
+
+// Synchronous fold with any pointer kinds.  All-device: one launch + stream
+// sync.  Otherwise: chunks of kChunkBytes, two pipeline slots on two
+// streams (H2D of chunk c+1 overlaps the kernel / D2H of chunk c).
+int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
+                unsigned flags, int device) {
+    const size_t es = dtype_size(dt);
+    if (!es) return fail(MI_E_INVALID, "unknown datatype");
+    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+    if (count == 0) return 0;
+    if (!out) return fail(MI_E_INVALID, "null output");
+    for (int i = 0; i < k; i++)
+        if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+
+    PtrKind kin[MI_MAX_INPUTS];
+    int pdev = -1;
+    bool all_dev = true;
+    for (int i = 0; i < k; i++) {
+        kin[i] = classify(inputs[i], &pdev);
+        all_dev = all_dev && kin[i] == PK_DEVICE;
+    }
+    const PtrKind kout = classify(out, &pdev);
+    all_dev = all_dev && kout == PK_DEVICE;
+    if (device < 0 && pdev >= 0) device = pdev;
+
+    DevCtx* d = nullptr;
+    int rc = get_ctx(device, &d);
+    if (rc) return rc;
+    int prev = 0;
+    MI_HIP(hipGetDevice(&prev));
+    if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+    struct Restore {
+        int dev, cur;
+        ~Restore() {
+            if (dev != cur) (void)hipSetDevice(dev);
+        }
+    } restore{prev, d->device};
+
+    if (all_dev) {
+        rc = launch_reduce(inputs, k, out, count, dt, op, flags, d->stream[0]);
+        if (rc) return rc;
+        MI_HIP(hipStreamSynchronize(d->stream[0]));
+        return 0;
+    }
+
+    // distinct host operands get a device staging buffer per slot; `out`
+    // reuses the buffer of the input it aliases (in-place inout)
+    int slot_of[MI_MAX_INPUTS + 1];
+    const void* host_ptr[MI_MAX_INPUTS + 1];
+    int nhost = 0;
+    for (int i = 0; i <= k; i++) {
+        const void* p = (i < k) ? inputs[i] : out;
+        const PtrKind kk = (i < k) ? kin[i] : kout;
+        slot_of[i] = -1;
+        if (kk == PK_DEVICE) continue;
+        for (int j = 0; j < nhost; j++)
+            if (host_ptr[j] == p) slot_of[i] = j;
+        if (slot_of[i] < 0) {
+            host_ptr[nhost] = p;
+            slot_of[i] = nhost++;
+        }
+    }
+    size_t chunk_elems = kChunkBytes / es;
+    chunk_elems -= chunk_elems % 16;  // keeps VCVTNEPS2BF16-tail split aligned (see below)
+    rc = ensure_scratch(d, (size_t)nhost, chunk_elems * es);
+    if (rc) return rc;
+
+    const size_t nchunks = (count + chunk_elems - 1) / chunk_elems;
+    for (size_t c = 0; c < nchunks; c++) {
+        const int s = (int)(c & 1);
+        hipStream_t st = d->stream[s];
+        const size_t off = c * chunk_elems;
+        const size_t n = std::min(chunk_elems, count - off);
+        const size_t bytes = n * es;
+        const void* din[MI_MAX_INPUTS];
+        std::vector<bool> loaded((size_t)nhost, false);
+        for (int i = 0; i < k; i++) {
+            if (slot_of[i] < 0) {
+                din[i] = static_cast<const char*>(inputs[i]) + off * es;
+            } else {
+                void* buf = d->dbuf[s][slot_of[i]];
+                if (!loaded[slot_of[i]]) {
+                    MI_HIP(hipMemcpyAsync(buf, static_cast<const char*>(inputs[i]) + off * es, bytes,
+                                          hipMemcpyHostToDevice, st));
+                    loaded[slot_of[i]] = true;
+                }
+                din[i] = buf;
+            }
+        }
+        void* dout = (slot_of[k] < 0) ? static_cast<char*>(out) + off * es : d->dbuf[s][slot_of[k]];
+        // The tail-truncation split is defined on the whole array: only the
+        // last chunk holds elements >= (count/16)*16, and chunk starts are
+        // multiples of 16, so the per-chunk split computed inside
+        // launch_reduce is the same split.
+        rc = launch_reduce(din, k, dout, n, dt, op, flags, st);
+        if (rc) return rc;
+        if (slot_of[k] >= 0)
+            MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, dout, bytes, hipMemcpyDeviceToHost, st));
+    }
+    MI_HIP(hipStreamSynchronize(d->stream[0]));
+    MI_HIP(hipStreamSynchronize(d->stream[1]));
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int mi_reduce(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,
+              void* stream) {
+    const void* ins[2] = {inout, in};
+    return launch_reduce(ins, 2, inout, count, dtype, op, flags, (hipStream_t)stream);
+}
+
+int mi_reduce_out(const void* in1, const void* in2, void* out, size_t count, int dtype, int op,
+                  unsigned flags, void* stream) {
+    const void* ins[2] = {in2, in1};
+    return launch_reduce(ins, 2, out, count, dtype, op, flags, (hipStream_t)stream);
+}
+
+int mi_reduce_multi(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                    unsigned flags, void* stream) {
+    if (!inputs) return fail(MI_E_INVALID, "null input list");
+    return launch_reduce(inputs, k, out, count, dtype, op, flags, (hipStream_t)stream);
+}
+
+int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,
+                   int device) {
+    const void* ins[2] = {inout, in};
+    return reduce_sync(ins, 2, inout, count, dtype, op, flags, device);
+}
+
+int mi_reduce_multi_sync(const void* const* inputs, int k, void* out, size_t count, int dtype,
+                         int op, unsigned flags, int device) {
+    if (!inputs) return fail(MI_E_INVALID, "null input list");
+    return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+}
+
+int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {
+    if (bytes == 0) return 0;
+    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) == 0;
+    if (!aligned) {
+        MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+        return 0;
+    }
+    const uint64_t nvec = bytes / 16;
+    const uint64_t tile = (uint64_t)kBlock * 4;
+    uint64_t blocks = (nvec + tile - 1) / tile;
+    const int cap = max_blocks();
+    if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
+    blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 0x7FFFFFFFull);
+    if (nontemporal)
+        hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                           static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), nvec);
+    else
+        hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                           static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), nvec);
+    MI_HIP(hipGetLastError());
+    return 0;
+}
+
+int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int device) {
+    if (bytes == 0) return 0;
+    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    int pdev = -1;
+    const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+    if (device < 0 && pdev >= 0) device = pdev;
+    DevCtx* d = nullptr;
+    int rc = get_ctx(device, &d);
+    if (rc) return rc;
+    if (ks == PK_DEVICE && kd == PK_DEVICE) {
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+        rc = mi_copy(src, dst, bytes, nontemporal, d->stream[0]);
+        if (!rc) {
+            hipError_t e = hipStreamSynchronize(d->stream[0]);
+            if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+        }
+        if (prev != d->device) (void)hipSetDevice(prev);
+        return rc;
+    }
+    MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
+    MI_HIP(hipStreamSynchronize(d->stream[0]));
+    return 0;
+}
+
+int mi_shard_range(size_t count, int rank, int world, size_t align, size_t* begin, size_t* end) {
+    if (world < 1 || rank < 0 || rank >= world || !begin || !end) return fail(MI_E_INVALID, "bad shard arguments");
+    if (align == 0) align = 256;
+    size_t per = (count + (size_t)world - 1) / (size_t)world;
+    per = (per + align - 1) / align * align;
+    size_t b = std::min(count, per * (size_t)rank);
+    size_t e = std::min(count, b + per);
+    *begin = b;
+    *end = e;
+    return 0;
+}
+
+const char* mi_reduction_to_str(int op) {
+    switch (op) {
+        case MI_OP_SUM: return "sum";
+        case MI_OP_PROD: return "prod";
+        case MI_OP_MIN: return "min";
+        case MI_OP_MAX: return "max";
+        case MI_OP_CUSTOM: return "custom";
+        default: return "unknown";
+    }
+}
+
+int mi_pointer_kind(const void* ptr, int* device) {
+    int dev = -1;
+    const int kind = (int)classify(ptr, &dev);
+    if (device) *device = dev;
+    return kind;
+}
+
+size_t mi_dtype_size(int dtype) { return dtype_size(dtype); }
+
+const char* mi_last_error(void) { return g_last_error.c_str(); }
+
+int mi_version(void) { return 100; }  // 0.1.0
+
+int mi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int mi_get_launch_config(int* block, int* unroll, int* max_blocks_out) {
+    if (block) *block = kBlock;
+    if (unroll) *unroll = kUnroll;
+    if (max_blocks_out) *max_blocks_out = max_blocks();
+    return 0;
+}
+
+int mi_set_max_blocks(int mb) {
+    if (mb < 0) return fail(MI_E_INVALID, "max_blocks must be >= 0");
+    g_max_blocks.store(mb, std::memory_order_relaxed);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,344 @@
+// reduce_kernels.hpp — CDNA4 (gfx950) element-wise reduction kernels.
+//
+// Device half of the MI355X-native replacement for oneCCL's local reduction:
+//   src/comp/comp.cpp:31-58      CCL_REDUCE (int / fp32 / fp64)
+//   src/comp/bf16/*              bf16 reduce (scalar / avx512f / avx512bf)
+//   src/comp/fp16/*              fp16 reduce (f16c / avx512f / avx512fp16)
+//   src/comp/comp.cpp:202-249    ccl_comp_batch_reduce (K-input fan-in,
+//                                optional fp32 keep-precision accumulate)
+//   src/kernels/kernels.cl:219-421  device in-place / out-of-place / fan-in
+//
+// Design: the op is a pure HBM stream with zero data reuse,
+// so there is no LDS and no MFMA.  Every lane moves 16-byte vectors
+// (global_load_dwordx4: one wave-instruction = 1 KiB, fully coalesced into
+// 128-byte lines), U independent vectors per input per lane so that
+// K*U*16 bytes per lane are in flight before the first use, non-temporal
+// stores for the output (written once, never re-read by this op).  bf16 /
+// fp16 are widened to fp32 in registers (a shift for bf16, v_cvt for fp16),
+// combined, and rounded back once per step (storage-precision chain) or
+// once at the end (fp32 accumulate).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace mi {
+
+enum : int { OP_SUM = 0, OP_PROD = 1, OP_MIN = 2, OP_MAX = 3 };
+
+// Semantic variant bits (same values as MI_F_* in include/mi_reduce.h).
+enum : unsigned {
+    V_INOUT_FIRST = 1u,  // min/max: MINPS/MAXPS(in, inout) order -> inout on NaN/tie
+    V_BF16_RNE = 2u,     // bf16 rounding: VCVTNEPS2BF16 (else truncate)
+    V_ACC_FP32 = 4u,     // lp fan-in accumulates in fp32, one rounding at the end
+    V_TAIL_TRUNC = 8u,   // with ACC|RNE: elements >= trunc_from truncate at the end
+};
+
+constexpr int kMaxInputs = 16;
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// storage tags for the two 16-bit float formats
+struct bf16_tag {};
+struct fp16_tag {};
+
+template <typename Tag>
+struct Tr {  // integers, float, double: storage == compute type
+    using S = Tag;
+    using C = Tag;
+    static constexpr bool lp = false;
+    static constexpr bool fp = std::is_floating_point<Tag>::value;
+};
+template <>
+struct Tr<bf16_tag> {
+    using S = uint16_t;
+    using C = float;
+    static constexpr bool lp = true;
+    static constexpr bool fp = true;
+};
+template <>
+struct Tr<fp16_tag> {
+    using S = uint16_t;
+    using C = float;
+    static constexpr bool lp = true;
+    static constexpr bool fp = true;
+};
+
+// Kernel arguments (passed by value in the kernarg segment).
+struct KArgs {
+    const void* in[kMaxInputs];  // in[0] = accumulator start (the `inout` role)
+    void* out;
+    uint64_t nvec;        // 16-byte vectors in the aligned body
+    uint64_t head;        // leading scalar elements (common misalignment)
+    uint64_t tail;        // trailing scalar elements
+    uint64_t count;       // total elements
+    uint64_t trunc_from;  // V_TAIL_TRUNC threshold (element index)
+    int k;                // number of inputs (runtime form)
+    int scalar_only;      // operands misaligned differently: element loop only
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// conversions (bit-exact restatements of the x86 instructions the reference
+// uses; see oracle/comp_oracle.c and oracle/ISA_CHECK.json)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(uint32_t v) { return __uint_as_float(v << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16_trunc(float f) { return __float_as_uint(f) >> 16; }
+
+// VCVTNEPS2BF16: zero/denormal -> signed zero, NaN -> quiet, else RNE.
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
+    const uint32_t u = __float_as_uint(f);
+    uint32_t r = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    r = ((u & 0x7FFFFFFFu) > 0x7F800000u) ? ((u >> 16) | 0x40u) : r;
+    r = ((u & 0x7F800000u) == 0u) ? ((u >> 16) & 0x8000u) : r;
+    return r;
+}
+
+// VCVTPH2PS: exact widening (v_cvt_f32_f16; fp16 denormals are on by default).
+__device__ __forceinline__ float fp16_to_f32(uint32_t h) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+}
+// VCVTPS2PH imm8=0: round to nearest even (v_cvt_f16_f32, default RNE mode).
+__device__ __forceinline__ uint32_t f32_to_fp16_rne(float f) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+template <typename Tag>
+__device__ __forceinline__ typename Tr<Tag>::C widen(typename Tr<Tag>::S s) {
+    if constexpr (std::is_same<Tag, bf16_tag>::value)
+        return bf16_to_f32(s);
+    else if constexpr (std::is_same<Tag, fp16_tag>::value)
+        return fp16_to_f32(s);
+    else
+        return s;
+}
+
+// round a compute value to storage: per-step / final rounding
+template <typename Tag, unsigned V>
+__device__ __forceinline__ typename Tr<Tag>::S narrow(typename Tr<Tag>::C c) {
+    if constexpr (std::is_same<Tag, bf16_tag>::value) {
+        if constexpr (V & V_BF16_RNE)
+            return (uint16_t)f32_to_bf16_rne(c);
+        else
+            return (uint16_t)f32_to_bf16_trunc(c);
+    } else if constexpr (std::is_same<Tag, fp16_tag>::value) {
+        return (uint16_t)f32_to_fp16_rne(c);
+    } else {
+        return c;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the reduction operator: acc' = op(in, acc)   (`in` role first, as in
+// CCL_REDUCE's std::min(in_buf[i], inout_buf[i]))
+// ---------------------------------------------------------------------------
+template <int OP, bool INOUT_FIRST, typename C>
+__device__ __forceinline__ C apply(C in, C acc) {
+    if constexpr (std::is_integral<C>::value) {
+        // wrap-around integer arithmetic (defined via unsigned)
+        using U = typename std::make_unsigned<C>::type;
+        using W = typename std::conditional<(sizeof(C) <= 4), uint32_t, uint64_t>::type;
+        if constexpr (OP == OP_SUM) return (C)(U)((W)(U)acc + (W)(U)in);
+        if constexpr (OP == OP_PROD) return (C)(U)((W)(U)acc * (W)(U)in);
+        if constexpr (OP == OP_MIN) return (acc < in) ? acc : in;
+        if constexpr (OP == OP_MAX) return (in < acc) ? acc : in;
+    } else {
+        if constexpr (OP == OP_SUM) return acc + in;
+        if constexpr (OP == OP_PROD) return acc * in;
+        if constexpr (OP == OP_MIN) {
+            if constexpr (INOUT_FIRST)
+                return (in < acc) ? in : acc;  // MINPS(in, inout)
+            else
+                return (acc < in) ? acc : in;  // std::min(in, inout)
+        }
+        if constexpr (OP == OP_MAX) {
+            if constexpr (INOUT_FIRST)
+                return (in > acc) ? in : acc;  // MAXPS(in, inout)
+            else
+                return (in < acc) ? acc : in;  // std::max(in, inout)
+        }
+    }
+}
+
+// one fold step in the variant's precision
+template <typename Tag, int OP, unsigned V>
+__device__ __forceinline__ typename Tr<Tag>::C step(typename Tr<Tag>::C x, typename Tr<Tag>::C acc) {
+    auto c = apply<OP, (V & V_INOUT_FIRST) != 0>(x, acc);
+    if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) c = widen<Tag>(narrow<Tag, V>(c));
+    return c;
+}
+
+// final rounding of the accumulator for element `idx`
+template <typename Tag, unsigned V>
+__device__ __forceinline__ typename Tr<Tag>::S finish(typename Tr<Tag>::C acc, uint64_t idx,
+                                                      uint64_t trunc_from) {
+    if constexpr (std::is_same<Tag, bf16_tag>::value && (V & V_TAIL_TRUNC)) {
+        return (idx >= trunc_from) ? (uint16_t)f32_to_bf16_trunc(acc)
+                                   : (uint16_t)f32_to_bf16_rne(acc);
+    } else {
+        return narrow<Tag, V>(acc);
+    }
+}
+
+template <int MEM>
+__device__ __forceinline__ u32x4 vload(const u32x4* p) {
+    if constexpr (MEM & 1)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+template <int MEM>
+__device__ __forceinline__ void vstore(u32x4* p, u32x4 v) {
+    if constexpr (MEM & 2)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <typename S>
+struct alignas(16) Pack {
+    S e[16 / sizeof(S)];
+};
+
+// scalar path for one element (head/tail/misaligned)
+template <typename Tag, int OP, unsigned V>
+__device__ __forceinline__ void reduce_elem(const KArgs& a, int k, uint64_t idx) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
+    for (int i = 1; i < k; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
+    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+}
+
+// One tile row: U vectors per lane at v0, v0+kBlock, ...  GUARD = last tile.
+template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, bool GUARD>
+__device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    constexpr int N = 16 / sizeof(S);
+    const uint64_t hb = a.head * sizeof(S);
+
+    C acc[U][N];
+    u32x4 cur[U];
+
+    const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[0]) + hb);
+    const u32x4* p1 =
+        reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[(KT == 2 || k >= 2) ? 1 : 0]) + hb);
+    // issue input 0 and input 1 loads back to back (2*U*16 B in flight per lane)
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = v0 + (uint64_t)j * kBlock;
+        if (!GUARD || v < a.nvec) {
+            u32x4 r = vload<MEM>(p0 + v);
+            Pack<S> p = __builtin_bit_cast(Pack<S>, r);
+#pragma unroll
+            for (int e = 0; e < N; e++) acc[j][e] = widen<Tag>(p.e[e]);
+        }
+    }
+    if (KT == 2 || k >= 2) {
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t v = v0 + (uint64_t)j * kBlock;
+            cur[j] = u32x4{0u, 0u, 0u, 0u};
+            if (!GUARD || v < a.nvec) cur[j] = vload<MEM>(p1 + v);
+        }
+    }
+
+    if constexpr (KT == 2) {
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            Pack<S> p = __builtin_bit_cast(Pack<S>, cur[j]);
+#pragma unroll
+            for (int e = 0; e < N; e++) acc[j][e] = step<Tag, OP, V>(widen<Tag>(p.e[e]), acc[j][e]);
+        }
+    } else {
+        for (int i = 1; i < k; i++) {
+            // prefetch input i+1 while combining input i
+            u32x4 nxt[U];
+            if (i + 1 < k) {
+                const u32x4* pn =
+                    reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[i + 1]) + hb);
+#pragma unroll
+                for (int j = 0; j < U; j++) {
+                    const uint64_t v = v0 + (uint64_t)j * kBlock;
+                    nxt[j] = u32x4{0u, 0u, 0u, 0u};
+                    if (!GUARD || v < a.nvec) nxt[j] = vload<MEM>(pn + v);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                Pack<S> p = __builtin_bit_cast(Pack<S>, cur[j]);
+#pragma unroll
+                for (int e = 0; e < N; e++) acc[j][e] = step<Tag, OP, V>(widen<Tag>(p.e[e]), acc[j][e]);
+            }
+            if (i + 1 < k) {
+#pragma unroll
+                for (int j = 0; j < U; j++) cur[j] = nxt[j];
+            }
+        }
+    }
+
+    u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = v0 + (uint64_t)j * kBlock;
+        if (!GUARD || v < a.nvec) {
+            Pack<S> p;
+#pragma unroll
+            for (int e = 0; e < N; e++)
+                p.e[e] = finish<Tag, V>(acc[j][e], a.head + v * N + e, a.trunc_from);
+            vstore<MEM>(po + v, __builtin_bit_cast(u32x4, p));
+        }
+    }
+}
+
+// Grid-stride over tiles of kBlock*U vectors.  Block 0 also does the
+// scalar head/tail (< 16 elements each).  `scalar_only` = operands with
+// different misalignments: plain element loop.
+template <typename Tag, int OP, unsigned V, int KT, int U, int MEM>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(KArgs a) {
+    const int k = (KT > 0) ? KT : a.k;
+    if (a.scalar_only) {
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.count;
+             i += (uint64_t)gridDim.x * kBlock)
+            reduce_elem<Tag, OP, V>(a, k, i);
+        return;
+    }
+    using S = typename Tr<Tag>::S;
+    constexpr int N = 16 / sizeof(S);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head) reduce_elem<Tag, OP, V>(a, k, threadIdx.x);
+        if (threadIdx.x < a.tail) reduce_elem<Tag, OP, V>(a, k, a.head + a.nvec * N + threadIdx.x);
+    }
+    const uint64_t tile = (uint64_t)kBlock * U;
+    const uint64_t stride = (uint64_t)gridDim.x * tile;
+    for (uint64_t base = (uint64_t)blockIdx.x * tile; base < a.nvec; base += stride) {
+        if (base + tile <= a.nvec)
+            reduce_tile<Tag, OP, V, KT, U, MEM, false>(a, k, base + threadIdx.x);
+        else
+            reduce_tile<Tag, OP, V, KT, U, MEM, true>(a, k, base + threadIdx.x);
+    }
+}
+
+// 16-byte vector copy with optional non-temporal stores (ccl_comp_copy).
+template <int MEM>
+__global__ __launch_bounds__(kBlock) void copy_kernel(const u32x4* __restrict__ src,
+                                                      u32x4* __restrict__ dst, uint64_t nvec) {
+    constexpr int U = 4;
+    const uint64_t tile = (uint64_t)kBlock * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec;
+         base += (uint64_t)gridDim.x * tile) {
+        u32x4 r[U];
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (base + (uint64_t)j * kBlock < nvec) r[j] = vload<MEM & 1>(src + base + (uint64_t)j * kBlock);
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (base + (uint64_t)j * kBlock < nvec) vstore<MEM & 2>(dst + base + (uint64_t)j * kBlock, r[j]);
+    }
+}
+
+}  // namespace mi

@@ -1,0 +1,113 @@
+"""CPU-side checks of the boundary: the libraries load without a GPU, export
+every symbol the public headers declare, and the pure-host functions behave
+(no device compute here)."""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from oneccl_amd import _lib
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _declared(header: str) -> list[str]:
+    text = (ROOT / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return re.findall(r"^\s*(?:const\s+)?[a-z_]+\s*\**\s+(mi_[a-z0-9_]+)\s*\(", text, flags=re.M)
+
+
+def _exported(lib: str) -> set[str]:
+    out = subprocess.run(["nm", "-D", "--defined-only", str(ROOT / "oneccl_amd" / "lib" / lib)],
+                         check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+@pytest.mark.parametrize("header,lib", [("mi_reduce.h", "libmi_reduce.so"), ("mi_ccl_comp.h", "libccl_comp_hip.so")])
+def test_every_declared_symbol_is_exported(header, lib):
+    decl = _declared(header)
+    assert len(decl) >= 8
+    missing = set(decl) - _exported(lib)
+    assert not missing, f"{lib} lacks {sorted(missing)}"
+
+
+def test_python_binding_covers_header():
+    assert {n for n, _, _ in _lib.MI_API} == set(_declared("mi_reduce.h"))
+    assert {n for n, _, _ in _lib.SHIM_API} == set(_declared("mi_ccl_comp.h"))
+
+
+def test_shim_exports_onecll_mangled_entry_points():
+    """The drop-in exports oneCCL's own C++ symbols (src/comp/comp.hpp:23-51)."""
+    out = subprocess.run(["nm", "-DC", "--defined-only", str(ROOT / "oneccl_amd/lib/libccl_comp_hip.so")],
+                         check=True, capture_output=True, text=True).stdout
+    want = [
+        "ccl_comp_reduce(ccl_sched*, void const*, unsigned long, void*, unsigned long*, ccl_datatype const&, "
+        "ccl::v1::reduction, void (*)(void const*, unsigned long, void*, unsigned long*, ccl::v1::datatype, "
+        "ccl::v1::fn_context const*), ccl::v1::fn_context const*)",
+        "ccl_comp_copy(void const*, void*, unsigned long, bool)",
+        "ccl_reduction_to_str(ccl::v1::reduction)",
+        "ccl_bf16_reduce(void const*, unsigned long, void*, unsigned long*, ccl::v1::reduction)",
+        "ccl_fp16_reduce(void const*, unsigned long, void*, unsigned long*, ccl::v1::reduction)",
+        "ccl_comp_batch_reduce(void const*, std::vector<unsigned long, std::allocator<unsigned long> > const&, "
+        "unsigned long, void*, unsigned long*, ccl_datatype const&, ccl::v1::reduction, void (*)(void const*, "
+        "unsigned long, void*, unsigned long*, ccl::v1::datatype, ccl::v1::fn_context const*), "
+        "ccl::v1::fn_context const*, int, float*, float*)",
+    ]
+    for w in want:
+        assert w in out, w
+
+
+def test_reduction_to_str_matches_reference():
+    # src/comp/comp.cpp:251-260
+    m = _lib.mi()
+    assert [m.mi_reduction_to_str(i).decode() for i in range(6)] == ["sum", "prod", "min", "max", "custom",
+                                                                      "unknown"]
+    s = _lib.shim()
+    assert [s.mi_ccl_reduction_to_str(i).decode() for i in range(5)] == ["sum", "prod", "min", "max", "custom"]
+
+
+def test_dtype_sizes():
+    m = _lib.mi()
+    assert [m.mi_dtype_size(i) for i in range(12)] == [1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 2]
+    assert m.mi_dtype_size(12) == 0
+
+
+def test_argument_errors_need_no_device():
+    m = _lib.mi()
+    assert m.mi_reduce(0, 0, 0, 9, 0, 0, None) == 0  # in_count == 0 is success (comp.cpp:132-134)
+    assert m.mi_reduce(0, 0, 10, 42, 0, 0, None) == -1
+    assert b"datatype" in m.mi_last_error()
+    assert m.mi_reduce(0, 0, 10, 9, 4, 0, None) == -1  # custom is host-only
+    arr = _lib.void_ptr_array([0] * 17)
+    assert m.mi_reduce_multi(arr, 17, 0, 10, 9, 0, 0, None) == -1
+
+
+@pytest.mark.parametrize("count", [0, 1, 255, 256, 1000, 1 << 28, (1 << 28) + 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_shard_range_partitions(count, world):
+    m = _lib.mi()
+    prev = 0
+    for r in range(world):
+        b, e = ctypes.c_size_t(), ctypes.c_size_t()
+        assert m.mi_shard_range(count, r, world, 256, ctypes.byref(b), ctypes.byref(e)) == 0
+        assert b.value == prev and e.value >= b.value
+        assert b.value % 256 == 0 or b.value == count
+        prev = e.value
+    assert prev == count
+
+
+def test_launch_config():
+    m = _lib.mi()
+    b, u, mb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert m.mi_get_launch_config(ctypes.byref(b), ctypes.byref(u), ctypes.byref(mb)) == 0
+    assert b.value % 64 == 0 and u.value >= 1 and mb.value >= 0
+    assert m.mi_set_max_blocks(-1) == -1
+    assert m.mi_set_max_blocks(mb.value) == 0
+
+
+def test_version():
+    assert _lib.mi().mi_version() >= 100

@@ -1,0 +1,228 @@
+"""GPU parity: the HIP kernels (through the C ABI, include/mi_reduce.h) against
+the CPU oracle (oracle/, a restatement of oneCCL src/comp) on the same seeded
+inputs.  Bar: bit-exact for every dtype and op (floating point: NaN payloads
+excepted — two NaNs compare equal — because x86 and CDNA produce different
+default NaNs; NaN-ness itself must match).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from oneccl_amd import _lib
+from oneccl_amd.comp import F_ACC_FP32, F_BF16_RNE, F_BF16_TAIL_TRUNC16, F_MINMAX_INOUT_FIRST, bf16_flags
+from tests.util import (ALL_DTYPES, BF16, DT_NAME, FP16, FP32, FP64, INT_DTYPES, OP_NAME, OPS, assert_same,
+                        from_dev, rand_array, to_dev)
+
+pytestmark = pytest.mark.gpu
+
+# reference semantics per dtype: (label, kernel flags, oracle bf16 impl, oracle fp16 impl)
+VARIANTS = {dt: [("ref", 0, oracle.BF16_AVX512BF, oracle.FP16_AVX512F)] for dt in INT_DTYPES + [FP32, FP64]}
+VARIANTS[BF16] = [("scalar", bf16_flags(0), oracle.BF16_SCALAR, 0),
+                  ("avx512f", bf16_flags(1), oracle.BF16_AVX512F, 0),
+                  ("avx512bf", bf16_flags(2), oracle.BF16_AVX512BF, 0)]
+VARIANTS[FP16] = [("avx512f", F_MINMAX_INOUT_FIRST, 0, oracle.FP16_AVX512F)]
+
+CASES = [(dt, op, v) for dt in ALL_DTYPES for op in OPS for v in VARIANTS[dt]]
+# element counts of the reference's functional tests (tests/functional/conf.cpp:51-53) + edges
+SIZES = [1, 17, 32771, 262144]
+
+
+def _sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+def gpu_reduce(a, b, dt, op, flags, off_in=0, off_io=0):
+    ta, pa = to_dev(a, offset_elems=off_in)
+    tb, pb = to_dev(b, offset_elems=off_io)
+    _lib.check(_lib.mi().mi_reduce(pa, pb, a.size, dt, op, flags, _stream()))
+    _sync()
+    return from_dev(tb, b, off_io)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("dt,op,var", CASES, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}-{v[0]}" for d, o, v in CASES])
+def test_reduce_inplace_vs_oracle(dt, op, var, n):
+    _, flags, bimpl, fimpl = var
+    a = rand_array(dt, n, seed=1000 + 17 * dt + op, op=op)
+    b = rand_array(dt, n, seed=2000 + 17 * dt + op, op=op)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, op, bimpl, fimpl)
+    got = gpu_reduce(a, b, dt, op, flags)
+    assert_same(got, exp, dt, f"{DT_NAME[dt]} {OP_NAME[op]} n={n}")
+
+
+@pytest.mark.parametrize("dt", [FP32, BF16, 0, FP64, FP16])
+@pytest.mark.parametrize("off_in,off_io", [(1, 1), (3, 3), (1, 0), (0, 2), (5, 7)])
+def test_misaligned_pointers(dt, off_in, off_io):
+    """Sub-buffer pointers (ring chunks at arbitrary element offsets): common
+    misalignment -> scalar head + vector body; different -> element loop."""
+    n = 4099
+    op = 0
+    var = VARIANTS[dt][-1]
+    a = rand_array(dt, n, seed=31 + dt)
+    b = rand_array(dt, n, seed=37 + dt)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, op, var[2], var[3])
+    got = gpu_reduce(a, b, dt, op, var[1], off_in, off_io)
+    assert_same(got, exp, dt, f"offsets {off_in},{off_io}")
+
+
+@pytest.mark.parametrize("dt,op", [(FP32, 0), (FP32, 3), (BF16, 0), (4, 1), (FP16, 2)])
+def test_reduce_out_of_place(dt, op):
+    n = 32771
+    var = VARIANTS[dt][-1]
+    a = rand_array(dt, n, seed=5, op=op)
+    b = rand_array(dt, n, seed=6, op=op)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, op, var[2], var[3])
+    ta, pa = to_dev(a)
+    tb, pb = to_dev(b)
+    to, po = to_dev(np.zeros_like(b))
+    _lib.check(_lib.mi().mi_reduce_out(pa, pb, po, n, dt, op, var[1], _stream()))
+    _sync()
+    assert_same(from_dev(to, b), exp, dt)
+    assert_same(from_dev(tb, b), b, dt, "in2 must be untouched")
+
+
+FANIN = [(FP32, 0, 3), (FP32, 0, 8), (FP32, 3, 16), (FP64, 1, 5), (4, 1, 8), (0, 0, 16), (7, 2, 4),
+         (BF16, 0, 8), (BF16, 2, 5), (FP16, 0, 8), (FP16, 3, 16)]
+
+
+@pytest.mark.parametrize("dt,op,k", FANIN, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}-k{k}" for d, o, k in FANIN])
+@pytest.mark.parametrize("n", [17, 262144 + 5])
+def test_fanin_storage_precision(dt, op, k, n):
+    """K-input fan-in == K-1 chained ccl_comp_reduce calls (the ring-chunk
+    arrival pattern; ccl_comp_batch_reduce non-keep mode, comp.cpp:236-245)."""
+    for var in VARIANTS[dt]:
+        ins = [rand_array(dt, n, seed=100 * j + dt, op=op) for j in range(k)]
+        exp = oracle.fanin(ins, dt, op, var[2], var[3])
+        holders = [to_dev(x) for x in ins]
+        to, po = to_dev(np.zeros_like(ins[0]))
+        arr = _lib.void_ptr_array([p for _, p in holders])
+        _lib.check(_lib.mi().mi_reduce_multi(arr, k, po, n, dt, op, var[1], _stream()))
+        _sync()
+        assert_same(from_dev(to, ins[0]), exp, dt, f"variant {var[0]}")
+
+
+@pytest.mark.parametrize("dt", [BF16, FP16])
+@pytest.mark.parametrize("op", OPS)
+@pytest.mark.parametrize("k", [2, 3, 8, 16])
+@pytest.mark.parametrize("rne,inout_first", [(True, False), (False, False), (True, True)])
+def test_fanin_fp32_accumulate(dt, op, k, rne, inout_first):
+    """bf16/fp16 fan-in with fp32 accumulation and one rounding at the end."""
+    if dt == FP16 and not rne:
+        pytest.skip("fp16 always rounds RNE")
+    n = 20011
+    ins = [rand_array(dt, n, seed=7 * j + op, op=op) for j in range(k)]
+    exp = oracle.lp_fanin_acc_fp32(ins, dt, op, rne, inout_first)
+    holders = [to_dev(x) for x in ins]
+    to, po = to_dev(np.zeros_like(ins[0]))
+    flags = F_ACC_FP32 | (F_BF16_RNE if rne else 0) | (F_MINMAX_INOUT_FIRST if inout_first else 0)
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, k, po, n, dt, op, flags, _stream()))
+    _sync()
+    assert_same(from_dev(to, ins[0]), exp, dt)
+
+
+@pytest.mark.parametrize("bimpl", [oracle.BF16_SCALAR, oracle.BF16_AVX512F, oracle.BF16_AVX512BF])
+@pytest.mark.parametrize("k", [1, 2, 4, 9])
+@pytest.mark.parametrize("n", [15, 16, 4099])
+def test_batch_reduce_keep_precision(bimpl, k, n):
+    """ccl_comp_batch_reduce(bf16_keep_precision_mode=1), comp.cpp:214-234,
+    including the truncated count%16 tail of the final array conversion."""
+    op = 0
+    ins = [rand_array(BF16, n, seed=900 + j) for j in range(k)]
+    packed = np.concatenate(ins)
+    offsets = [j * n for j in range(k)]
+    exp = ins[0].copy()
+    oracle.batch_reduce(packed, offsets, n, exp, BF16, op, 1, bimpl, 0)
+    flags = F_ACC_FP32 | ((F_BF16_RNE | F_BF16_TAIL_TRUNC16) if bimpl == oracle.BF16_AVX512BF else 0)
+    holders = [to_dev(x) for x in ins]
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, k, holders[0][1], n, BF16, op, flags, _stream()))
+    _sync()
+    assert_same(from_dev(holders[0][0], ins[0]), exp, BF16)
+
+
+def test_zero_count_and_errors():
+    m = _lib.mi()
+    assert m.mi_reduce(0, 0, 0, FP32, 0, 0, _stream()) == 0
+    assert m.mi_reduce(0, 0, 10, 99, 0, 0, _stream()) < 0
+    assert m.mi_reduce(0, 0, 10, FP32, 4, 0, _stream()) < 0
+    assert b"reduction" in m.mi_last_error()
+
+
+def test_shards_compose():
+    """Element-range sharding: reducing each shard separately
+    gives the whole-array result bit for bit."""
+    n = 1_000_003
+    a = rand_array(FP32, n, seed=1)
+    b = rand_array(FP32, n, seed=2)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, FP32, 0)
+    ta, pa = to_dev(a)
+    tb, pb = to_dev(b)
+    m = _lib.mi()
+    for world in (1, 2, 4, 8):
+        tb.copy_(to_dev(b)[0])
+        for r in range(world):
+            lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+            _lib.check(m.mi_shard_range(n, r, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
+            _lib.check(m.mi_reduce(pa + 4 * lo.value, pb + 4 * lo.value, hi.value - lo.value, FP32, 0, 0, _stream()))
+        _sync()
+        assert_same(from_dev(tb, b), exp, FP32, f"world={world}")
+
+
+# ---- BASELINE.json full-size configurations --------------------------------
+
+def test_full_c2_fp32_sum_1gib():
+    """C2: 2-input fp32 sum, 1 GiB device-resident — bit-exact vs the oracle."""
+    n = (1 << 30) // 4
+    a = rand_array(FP32, n, seed=0xC0FFEE, specials=False)
+    b = rand_array(FP32, n, seed=0xBEEF, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    got = gpu_reduce(a, b, FP32, 0, 0)
+    assert_same(got, exp, FP32, "C2")
+
+
+@pytest.mark.parametrize("dt", [BF16, FP16])
+def test_full_c3_lp_sum_256mib(dt):
+    """C3: fp16 / bf16 sum with fp32 accumulate, 256 MiB — bit-exact (2-input:
+    one rounding of the fp32 sum, as the reference's avx512bf / avx512f)."""
+    n = (256 << 20) // 2
+    a = rand_array(dt, n, seed=0x1234, specials=False)
+    b = rand_array(dt, n, seed=0x4321, specials=False)
+    exp = b.copy()
+    bimpl, fimpl = (oracle.BF16_AVX512BF, 0) if dt == BF16 else (0, oracle.FP16_AVX512F)
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, bimpl, fimpl)
+    flags = bf16_flags(2) if dt == BF16 else F_MINMAX_INOUT_FIRST
+    got = gpu_reduce(a, b, dt, 0, flags)
+    assert_same(got, exp, dt, "C3")
+
+
+def test_full_c4_fanin8_fp32_1gib():
+    """C4: 8-input fp32 sum fan-in over 1 GiB buffers == 7 chained reduces."""
+    n = (1 << 30) // 4
+    ins = [rand_array(FP32, n, seed=0xA0 + j, specials=False) for j in range(8)]
+    exp = ins[0].copy()
+    for x in ins[1:]:
+        oracle.comp_reduce_mt(x, exp, FP32, 0, 8)
+    holders = [to_dev(x) for x in ins]
+    del ins[1:]
+    to, po = to_dev(np.zeros(1, np.float32), pad_elems=n - 1)
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, 8, po, n, FP32, 0, 0, _stream()))
+    _sync()
+    got = to.cpu().numpy().view(np.float32)
+    assert_same(got, exp, FP32, "C4")

@@ -1,0 +1,112 @@
+"""Shared helpers for the parity tests: seeded inputs (with the special
+values the reference's semantics distinguish), numpy<->device transfer and
+the comparison rule (bit-exact; for floating point, two NaNs of any payload
+compare equal: x86 and CDNA generate different default NaNs)."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+
+# ccl::datatype ids
+INT_DTYPES = [0, 1, 2, 3, 4, 5, 6, 7]
+FP16, FP32, FP64, BF16 = 8, 9, 10, 11
+ALL_DTYPES = INT_DTYPES + [FP16, FP32, FP64, BF16]
+OPS = [0, 1, 2, 3]
+DT_NAME = {0: "int8", 1: "uint8", 2: "int16", 3: "uint16", 4: "int32", 5: "uint32", 6: "int64", 7: "uint64",
+           8: "float16", 9: "float32", 10: "float64", 11: "bfloat16"}
+OP_NAME = {0: "sum", 1: "prod", 2: "min", 3: "max"}
+
+F32_SPECIALS = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, -np.nan, 1e-40, -1e-40, 1e-45,
+                         3.4e38, -3.4e38, 1.17549435e-38, 65504.0, 6.1e-5, 5.96e-8, 2.0 ** -126],
+                        dtype=np.float32)
+
+
+def rand_array(dtype: int, n: int, seed: int, op: int = 0, specials: bool = True) -> np.ndarray:
+    """Seeded input of ccl datatype `dtype` (storage dtype as in oracle.NP_DTYPE)."""
+    rng = np.random.default_rng(seed)
+    st = oracle.NP_DTYPE[dtype]
+    if dtype in INT_DTYPES:
+        info = np.iinfo(st)
+        if op == 1:  # keep products from being all-zero quickly; wraps still exercised
+            a = rng.integers(-3, 4, size=n).astype(np.int64)
+            if info.min == 0:
+                a = np.abs(a)
+            a = a.astype(st)
+        else:
+            a = rng.integers(info.min, info.max, size=n, endpoint=True, dtype=st)
+        if specials and n > 8:
+            idx = rng.choice(n, size=min(n, 8), replace=False)
+            a[idx[:4]] = info.min
+            a[idx[4:]] = info.max
+        return a
+    if dtype == FP64:
+        a = rng.standard_normal(n) * (10.0 ** rng.integers(-3, 4, size=n))
+        if specials and n > 40:
+            idx = rng.choice(n, size=len(F32_SPECIALS), replace=False)
+            a[idx] = F32_SPECIALS.astype(np.float64)
+            a[idx[0]] = 1e-310  # fp64 denormal
+        return a
+    f = (rng.standard_normal(n) * (2.0 ** rng.integers(-8, 9, size=n))).astype(np.float32)
+    if specials and n > 40:
+        idx = rng.choice(n, size=len(F32_SPECIALS), replace=False)
+        f[idx] = F32_SPECIALS
+    if dtype == FP32:
+        return f
+    if dtype == BF16:
+        b = oracle.f32_to_bf16(f, rne=True)
+        if specials and n > 40:  # bf16 denormals and tiny values
+            idx = rng.choice(n, size=6, replace=False)
+            b[idx] = np.array([0x0001, 0x8001, 0x007F, 0x0080, 0x7F7F, 0xFF7F], np.uint16)
+        return b
+    # fp16
+    h = oracle.f32_to_fp16(np.clip(f, -60000, 60000))
+    if specials and n > 40:
+        idx = rng.choice(n, size=8, replace=False)
+        h[idx] = np.array([0x0001, 0x8001, 0x03FF, 0x0400, 0x7BFF, 0xFBFF, 0x7C00, 0x7E00], np.uint16)
+    return h
+
+
+def is_nan_bits(a: np.ndarray, dtype: int) -> np.ndarray:
+    if dtype == BF16:
+        return ((a & 0x7F80) == 0x7F80) & ((a & 0x007F) != 0)
+    if dtype == FP16:
+        return ((a & 0x7C00) == 0x7C00) & ((a & 0x03FF) != 0)
+    if dtype in (FP32, FP64):
+        return np.isnan(a)
+    return np.zeros(a.shape, bool)
+
+
+def assert_same(got: np.ndarray, exp: np.ndarray, dtype: int, what: str = "") -> None:
+    """Bit-exact, NaN-payload-agnostic comparison."""
+    assert got.shape == exp.shape
+    gb = got.view(np.uint8).reshape(got.size, -1)
+    eb = exp.view(np.uint8).reshape(exp.size, -1)
+    diff = np.any(gb != eb, axis=1)
+    nn = is_nan_bits(got, dtype) & is_nan_bits(exp, dtype)
+    bad = diff & ~nn
+    if bad.any():
+        i = np.flatnonzero(bad)
+        raise AssertionError(f"{what}: {len(i)} of {got.size} elements differ; first at {i[:5].tolist()}: "
+                             f"got {got[i[:5]].tolist()} expected {exp[i[:5]].tolist()}")
+
+
+# ---- device transfer (torch is plumbing only) ----------------------------
+_SIGNED = {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}
+
+
+def to_dev(a: np.ndarray, pad_elems: int = 0, offset_elems: int = 0):
+    """Copy to a fresh device buffer; returns (tensor_holder, device_ptr).
+    `offset_elems` shifts the data inside the buffer to test misaligned
+    pointers."""
+    import torch
+    es = a.itemsize
+    raw = np.zeros(a.size + pad_elems + offset_elems, a.dtype)
+    raw[offset_elems:offset_elems + a.size] = a
+    t = torch.from_numpy(raw.view(_SIGNED[es])).cuda()
+    return t, t.data_ptr() + offset_elems * es
+
+
+def from_dev(t, like: np.ndarray, offset_elems: int = 0) -> np.ndarray:
+    host = t.cpu().numpy().view(like.dtype)
+    return host[offset_elems:offset_elems + like.size].copy()

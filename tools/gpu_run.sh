@@ -1,0 +1,61 @@
+#!/usr/bin/env bash
+# GPU-box session script: every GPU step under its own timeout; stop at the
+# first fault / abort / segfault / timeout (exit codes 124 134 137 139 or a
+# signal), continue past ordinary test failures (pytest exit 1).
+# Usage: tools/gpu_run.sh STEP [STEP ...]   steps: host tests sweep bench prof pmc benchall
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # run NAME TIMEOUT CMD...
+    local name=$1 t=$2; shift 2
+    echo "=== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+    case $rc in
+        0|1) return 0 ;;       # ok / test failures: keep going
+        *) echo "STOP: $name exited $rc" | tee -a "$OUT/steps.log"; exit $rc ;;
+    esac
+}
+
+for step in "$@"; do
+    case $step in
+        host)
+            { nproc; lscpu; rocm-smi --showproductname --showmeminfo vram 2>&1 | head -40; } > "$OUT/host.txt" 2>&1 ;;
+        tests)
+            run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider ;;
+        tests_fast)
+            run pytest_gpu 600 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider -k "not full" ;;
+        smoke)
+            run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        sweep)
+            run sweep 300 ./tools/reduce_sweep 1024 3 10 ;;
+        bench)
+            run bench 600 python bench.py ;;
+        benchall)
+            for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
+                run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
+            done ;;
+        prof)
+            (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$GRAFT_REPO_ROOT/$OUT/prof" -o bench -- \
+                python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg \
+                > "$GRAFT_REPO_ROOT/$OUT/prof.out" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
+            rc=$?; echo "=== prof rc=$rc" | tee -a "$OUT/steps.log"
+            [ $rc -eq 0 ] || exit $rc ;;
+        pmc)
+            for ctr in FETCH_SIZE WRITE_SIZE; do
+                (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv \
+                    -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o bench -- \
+                    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-host-leg \
+                    > "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err")
+                rc=$?; echo "=== pmc $ctr rc=$rc" | tee -a "$OUT/steps.log"
+                [ $rc -eq 0 ] || exit $rc
+            done ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "=== all steps done" | tee -a "$OUT/steps.log"

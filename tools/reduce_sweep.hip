@@ -1,0 +1,130 @@
+// reduce_sweep.hip — launch-geometry / memory-policy sweep of the fp32 sum
+// reduce kernel (the same template the library instantiates) on a 1 GiB
+// bucket, against two known-good streaming references measured on the same
+// device: hipMemcpy D2D and the library's own copy kernel.
+//
+// Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
+// Output: one JSON object per variant on stdout.
+//   reduce_sweep [bucket_MiB=1024] [rounds=5] [reps=10]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../oneccl_amd/csrc/reduce_kernels.hpp"
+
+using namespace mi;
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e = (x);                                                              \
+        if (e != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+struct Variant {
+    std::string name;
+    double traffic;  // bytes per launch
+    std::function<void(hipStream_t)> run;
+    std::vector<float> ms;
+};
+
+template <int U, int MEM>
+void add_reduce(std::vector<Variant>& vs, KArgs a, int cap, double traffic) {
+    const uint64_t tile = (uint64_t)kBlock * U;
+    uint64_t blocks = (a.nvec + tile - 1) / tile;
+    if (cap > 0) blocks = std::min<uint64_t>(blocks, cap);
+    char name[128];
+    snprintf(name, sizeof name, "reduce U=%d mem=%d grid=%s%llu", U, MEM, cap ? "cap" : "", (unsigned long long)blocks);
+    vs.push_back({name, traffic, [a, blocks](hipStream_t s) {
+                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, 2, U, MEM>), dim3((unsigned)blocks),
+                                         dim3(kBlock), 0, s, a);
+                  }, {}});
+}
+
+int main(int argc, char** argv) {
+    const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const size_t bytes = mib << 20;
+    const size_t n = bytes / 4;
+    float *in, *io, *cp;
+    CK(hipMalloc(&in, bytes));
+    CK(hipMalloc(&io, bytes));
+    CK(hipMalloc(&cp, bytes));
+    CK(hipMemset(in, 0x3c, bytes));  // ~0.0115f: finite, non-zero
+    CK(hipMemset(io, 0x3c, bytes));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+
+    KArgs a{};
+    a.in[0] = io;
+    a.in[1] = in;
+    a.out = io;
+    a.k = 2;
+    a.count = n;
+    a.nvec = n / 4;
+    a.trunc_from = n;
+    const double t3 = 3.0 * bytes;
+
+    std::vector<Variant> vs;
+    const int caps[] = {0, 256, 512, 1024, 2048, 4096, 8192};
+    for (int cap : caps) {
+        add_reduce<1, 2>(vs, a, cap, t3);
+        add_reduce<2, 2>(vs, a, cap, t3);
+        add_reduce<4, 0>(vs, a, cap, t3);
+        add_reduce<4, 1>(vs, a, cap, t3);
+        add_reduce<4, 2>(vs, a, cap, t3);
+        add_reduce<4, 3>(vs, a, cap, t3);
+        add_reduce<8, 2>(vs, a, cap, t3);
+    }
+    vs.push_back({"hipMemcpyAsync D2D", 2.0 * bytes,
+                  [=](hipStream_t st) { (void)hipMemcpyAsync(cp, in, bytes, hipMemcpyDeviceToDevice, st); }, {}});
+    for (int mem : {0, 2}) {
+        const uint64_t nvec = bytes / 16;
+        const uint64_t blocks = (nvec + kBlock * 4 - 1) / (kBlock * 4);
+        vs.push_back({mem ? "copy_kernel nt-store" : "copy_kernel plain", 2.0 * bytes, [=](hipStream_t st) {
+                          if (mem)
+                              hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                                                 (const u32x4*)in, (u32x4*)cp, nvec);
+                          else
+                              hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                                                 (const u32x4*)in, (u32x4*)cp, nvec);
+                      }, {}});
+    }
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto& v : vs) v.run(s);  // warm every variant
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vs) {
+            for (int i = 0; i < reps; i++) {
+                CK(hipEventRecord(e0, s));
+                v.run(s);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        }
+        fprintf(stderr, "round %d/%d done\n", r + 1, rounds);
+    }
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
+        printf("{\"variant\": \"%s\", \"bucket_MiB\": %zu, \"median_ms\": %.5f, \"best_ms\": %.5f, "
+               "\"median_GBps\": %.1f, \"best_GBps\": %.1f, \"frac_of_8TBps\": %.4f}\n",
+               v.name.c_str(), mib, med, best, v.traffic / (med * 1e-3) / 1e9, v.traffic / (best * 1e-3) / 1e9,
+               v.traffic / (med * 1e-3) / 8e12);
+    }
+    return 0;
+}
