@@ -44,7 +44,7 @@ int hip_fail(hipError_t e, const char* what) {
 // launch configuration
 // ---------------------------------------------------------------------------
 constexpr int kUnroll = 4;  // 16-byte vectors per lane per input per tile
-constexpr int kMem = 2;     // plain loads, non-temporal stores
+constexpr int kMem = 3;     // non-temporal loads and stores (sweep: profiles/round1_sweep.jsonl)
 
 std::atomic<int> g_max_blocks{-1};  // -1 = not yet read from env; 0 = no cap
 

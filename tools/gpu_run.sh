@@ -33,6 +33,8 @@ for step in "$@"; do
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         sweep)
             run sweep 300 ./tools/reduce_sweep 1024 3 10 ;;
+        policy)
+            run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
             run bench 600 python bench.py ;;
         benchall)

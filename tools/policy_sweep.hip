@@ -1,0 +1,188 @@
+// policy_sweep.hip — experiment: fp32 2-input sum over a 1 GiB bucket with
+// one-shot grids, varying block size, vectors per lane, the load/store
+// cache-policy bits (buffer ops: aux bit0 = sc0, bit1 = nt, bit4 = sc1) and
+// the block -> tile mapping (linear vs XCD-contiguous).  Interleaved rounds,
+// one process.  Output: one JSON object per variant.
+//   policy_sweep [bucket_MiB=1024] [rounds=5] [reps=10]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e = (x);                                                              \
+        if (e != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// MAP 0: tile = blockIdx.x.  MAP 1: blocks b, b+8, ... (one XCD under the
+// observed round-robin dispatch) take a contiguous 1/8 of the tiles.
+template <int MAP>
+__device__ __forceinline__ uint32_t tile_of(uint32_t b, uint32_t g) {
+    if constexpr (MAP == 0) return b;
+    const uint32_t per = g / 8;  // host guarantees g % 8 == 0
+    return (b % 8) * per + b / 8;
+}
+
+template <int B, int U, int LP, int SP, int MAP>
+__global__ __launch_bounds__(B) void k_buffer(const float* in, float* io, uint32_t tiles) {
+    const uint32_t t = tile_of<MAP>(blockIdx.x, gridDim.x);
+    if (t >= tiles) return;
+    const size_t tb = (size_t)B * U * 16;
+    const char* pin = reinterpret_cast<const char*>(in) + t * tb;
+    char* pio = reinterpret_cast<char*>(io) + t * tb;
+    __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void*)pin, (short)0, (int)tb, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)pio, (short)0, (int)tb, 0x00020000);
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) a[j] = __builtin_amdgcn_raw_buffer_load_b128(ro, (threadIdx.x + j * B) * 16, 0, LP);
+#pragma unroll
+    for (int j = 0; j < U; j++) b[j] = __builtin_amdgcn_raw_buffer_load_b128(ri, (threadIdx.x + j * B) * 16, 0, LP);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        f32x4 x = __builtin_bit_cast(f32x4, a[j]) + __builtin_bit_cast(f32x4, b[j]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), ro, (threadIdx.x + j * B) * 16, 0, SP);
+    }
+}
+
+template <int B, int U, int NT, int MAP>
+__global__ __launch_bounds__(B) void k_global(const u32x4* in, u32x4* io, uint32_t tiles) {
+    const uint32_t t = tile_of<MAP>(blockIdx.x, gridDim.x);
+    if (t >= tiles) return;
+    const size_t base = (size_t)t * B * U + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) a[j] = NT ? __builtin_nontemporal_load(io + base + j * B) : io[base + j * B];
+#pragma unroll
+    for (int j = 0; j < U; j++) b[j] = NT ? __builtin_nontemporal_load(in + base + j * B) : in[base + j * B];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        f32x4 x = __builtin_bit_cast(f32x4, a[j]) + __builtin_bit_cast(f32x4, b[j]);
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x), io + base + j * B);
+    }
+}
+
+struct Variant {
+    std::string name;
+    std::function<void(hipStream_t)> run;
+    std::vector<float> ms;
+};
+
+size_t g_nvec;
+const float* g_in;
+float* g_io;
+
+template <int B, int U, int LP, int SP, int MAP>
+void addb(std::vector<Variant>& vs) {
+    const uint32_t tiles = (uint32_t)(g_nvec / (B * U));
+    uint32_t grid = tiles;
+    if (MAP) grid = (tiles + 7) / 8 * 8;
+    char name[128];
+    snprintf(name, sizeof name, "buffer B=%d U=%d ld=%d st=%d map=%d", B, U, LP, SP, MAP);
+    const float* in = g_in;
+    float* io = g_io;
+    vs.push_back({name, [=](hipStream_t s) {
+                      hipLaunchKernelGGL((k_buffer<B, U, LP, SP, MAP>), dim3(grid), dim3(B), 0, s, in, io, tiles);
+                  }, {}});
+}
+
+template <int B, int U, int NT, int MAP>
+void addg(std::vector<Variant>& vs) {
+    const uint32_t tiles = (uint32_t)(g_nvec / (B * U));
+    uint32_t grid = tiles;
+    if (MAP) grid = (tiles + 7) / 8 * 8;
+    char name[128];
+    snprintf(name, sizeof name, "global B=%d U=%d nt=%d map=%d", B, U, NT, MAP);
+    const u32x4* in = (const u32x4*)g_in;
+    u32x4* io = (u32x4*)g_io;
+    vs.push_back({name, [=](hipStream_t s) {
+                      hipLaunchKernelGGL((k_global<B, U, NT, MAP>), dim3(grid), dim3(B), 0, s, in, io, tiles);
+                  }, {}});
+}
+
+int main(int argc, char** argv) {
+    const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const size_t bytes = mib << 20;
+    float *in, *io;
+    CK(hipMalloc(&in, bytes));
+    CK(hipMalloc(&io, bytes));
+    CK(hipMemset(in, 0x3c, bytes));
+    CK(hipMemset(io, 0x3c, bytes));
+    g_nvec = bytes / 16;
+    g_in = in;
+    g_io = io;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+
+    std::vector<Variant> vs;
+    addg<256, 4, 1, 0>(vs);  // == the library's current best
+    addg<256, 4, 1, 1>(vs);
+    addg<512, 4, 1, 0>(vs);
+    addg<1024, 4, 1, 0>(vs);
+    addg<256, 2, 1, 0>(vs);
+    addg<256, 8, 1, 0>(vs);
+    addg<512, 2, 1, 0>(vs);
+    addg<1024, 2, 1, 0>(vs);
+    addg<1024, 1, 1, 0>(vs);
+    addg<512, 8, 1, 0>(vs);
+    addg<256, 16, 1, 0>(vs);
+    addb<256, 4, 2, 2, 0>(vs);
+    addb<256, 4, 3, 2, 0>(vs);
+    addb<256, 4, 18, 2, 0>(vs);
+    addb<256, 4, 19, 2, 0>(vs);
+    addb<256, 4, 16, 2, 0>(vs);
+    addb<256, 4, 2, 18, 0>(vs);
+    addb<256, 4, 2, 3, 0>(vs);
+    addb<256, 4, 2, 19, 0>(vs);
+    addb<256, 4, 2, 16, 0>(vs);
+    addb<256, 4, 2, 0, 0>(vs);
+    addb<256, 4, 0, 2, 0>(vs);
+    addb<256, 4, 2, 2, 1>(vs);
+    addb<512, 4, 2, 2, 0>(vs);
+    addb<1024, 4, 2, 2, 0>(vs);
+    addb<256, 8, 2, 2, 0>(vs);
+    addb<512, 8, 2, 2, 0>(vs);
+    addb<1024, 2, 2, 2, 0>(vs);
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto& v : vs) v.run(s);
+    CK(hipStreamSynchronize(s));
+    CK(hipGetLastError());
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vs) {
+            for (int i = 0; i < reps; i++) {
+                CK(hipEventRecord(e0, s));
+                v.run(s);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        }
+        fprintf(stderr, "round %d/%d\n", r + 1, rounds);
+    }
+    const double traffic = 3.0 * bytes;
+    for (auto& v : vs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
+        printf("{\"variant\": \"%s\", \"median_ms\": %.5f, \"best_ms\": %.5f, \"median_GBps\": %.1f, "
+               "\"best_GBps\": %.1f}\n",
+               v.name.c_str(), med, best, traffic / (med * 1e-3) / 1e9, traffic / (best * 1e-3) / 1e9);
+    }
+    return 0;
+}
