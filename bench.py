@@ -132,6 +132,33 @@ def cpu_baseline(cfg, seconds):
     }
 
 
+def plan(n_total, es, rank, world, scaling):
+    """Elements this rank reduces per step, its first element, and the bytes
+    all ranks reduce per step.  weak: every rank owns a full bucket (the
+    element range of a world x bucket job, sharded); strong: one bucket split
+    by element range (mi_shard_range, 256-element aligned)."""
+    if scaling == "weak":
+        return n_total, rank * n_total, n_total * es * world
+    import ctypes
+
+    from oneccl_amd import _lib
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(_lib.mi().mi_shard_range(n_total, rank, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
+    return hi.value - lo.value, lo.value, n_total * es
+
+
+def max_over_ranks(vals, world, device):
+    """Max of each value over all ranks (the driver's contract: the slowest
+    rank's time is the job's time)."""
+    if world <= 1:
+        return list(vals)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
 def main():
     args = parse()
     import torch
@@ -151,13 +178,7 @@ def main():
     cfg = CONFIGS[args.config]
     desc, dt, es, op, k, bucket, flags = cfg
     n_total = bucket // es
-    if args.scaling == "weak":
-        n = n_total
-    else:
-        import ctypes
-        lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
-        _lib.check(_lib.mi().mi_shard_range(n_total, rank, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
-        n = hi.value - lo.value
+    n, _, total_bytes = plan(n_total, es, rank, world, args.scaling)
 
     m = _lib.mi()
     tdt = torch_dtype(dt)
@@ -203,15 +224,9 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     avg_kern_ms = statistics.mean(kern_ms)
 
-    if world > 1:
-        t = torch.tensor([elapsed, avg_kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, avg_kern_ms_max = t.tolist()
-    else:
-        avg_kern_ms_max = avg_kern_ms
+    elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, "cuda")
 
     units_per_rank = n * es  # bucket bytes this rank reduced per step
-    total_bytes = units_per_rank * world if args.scaling == "weak" else n_total * es
     value = total_bytes * args.steps / elapsed / GiB
     traffic_per_launch = (k + 1) * n * es  # read k inputs, write 1 (algorithmic)
     achieved = traffic_per_launch / (avg_kern_ms / 1e3) / 1e9

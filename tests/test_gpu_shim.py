@@ -1,0 +1,271 @@
+"""The drop-in src/comp (libccl_comp_hip.so: oneCCL's own ccl_comp_* entry
+points over the HIP kernels) driven the way src/sched drives it —
+synchronous calls on host staging buffers, device buffers or a mix — checked
+against the oracle under the same bf16/fp16 impl types the shim selected
+(CPUID + CCL_BF16 / CCL_FP16, src/common/env/env.cpp:711-720)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from oneccl_amd import _lib, comp
+from tests import kat
+from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, FP32, OP_NAME, OPS, assert_same, from_dev, rand_array, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _reset_env():
+    saved = {k: os.environ.get(k) for k in ("CCL_BF16", "CCL_FP16")}
+    yield
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    comp.env_reload()
+
+
+def impls():
+    b, f = comp.impl_types()
+    return int(b), int(f)
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+@pytest.mark.parametrize("dt", ALL_DTYPES, ids=[DT_NAME[d] for d in ALL_DTYPES])
+@pytest.mark.parametrize("op", OPS, ids=[OP_NAME[o] for o in OPS])
+def test_comp_reduce_host_buffers(dt, op):
+    """recv_reduce_entry's call: host comm_buf into a host accumulator."""
+    n = 32771
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=11 + dt, op=op)
+    b = rand_array(dt, n, seed=12 + dt, op=op)
+    exp = b.copy()
+    oc_ref = oracle.comp_reduce(a, exp, dt, op, b_impl, f_impl)
+    oc = comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype(dt), comp.reduction(op))
+    assert_same(b, exp, dt)
+    assert oc == oc_ref  # out_count written only by bf16/fp16 (bf16.cpp:94-96, fp16.cpp:48-50)
+
+
+@pytest.mark.parametrize("where", ["device", "pinned", "in_host_inout_dev", "in_dev_inout_host"])
+@pytest.mark.parametrize("dt", [FP32, BF16, FP16, 6])
+def test_comp_reduce_pointer_kinds(where, dt):
+    import torch
+    n = 100_000
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=3)
+    b = rand_array(dt, n, seed=4)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, 0, b_impl, f_impl)
+    if where == "device":
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+        got = from_dev(tb, b)
+    elif where == "pinned":
+        ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        comp.comp_reduce(ha.data_ptr(), n, hb.data_ptr(), comp.datatype(dt), comp.reduction.sum)
+        got = hb.numpy().view(b.dtype)
+    elif where == "in_host_inout_dev":
+        tb, pb = to_dev(b)
+        comp.comp_reduce(ptr(a), n, pb, comp.datatype(dt), comp.reduction.sum)
+        got = from_dev(tb, b)
+    else:
+        ta, pa = to_dev(a)
+        got = b.copy()
+        comp.comp_reduce(pa, n, ptr(got), comp.datatype(dt), comp.reduction.sum)
+    assert_same(got, exp, dt, where)
+
+
+@pytest.mark.parametrize("dt", [FP32, BF16])
+def test_large_host_buffer_pipelined(dt):
+    """> 1 staging chunk (32 MiB): the H2D / kernel / D2H pipeline over two
+    streams must produce the whole-array result."""
+    n = (80 << 20) // 4 + 12345
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=21, specials=False)
+    b = rand_array(dt, n, seed=22, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+    comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype(dt), comp.reduction.sum)
+    assert_same(b, exp, dt)
+
+
+@pytest.mark.parametrize("setting,impl", [("scalar", 0), ("avx512f", 1), ("avx512bf", 2)])
+def test_ccl_bf16_env_selects_semantics(setting, impl):
+    """CCL_BF16=<impl> (doc/rst/source/env-variables.rst CCL_BF16) changes the
+    bit-level result exactly as it changes the reference's."""
+    os.environ["CCL_BF16"] = setting
+    comp.env_reload()
+    assert impls()[0] == impl
+    n = 4099
+    for op in OPS:
+        a = rand_array(BF16, n, seed=40 + op, op=op)
+        b = rand_array(BF16, n, seed=50 + op, op=op)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, BF16, op, impl)
+        comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype.bfloat16, comp.reduction(op))
+        assert_same(b, exp, BF16, f"{setting} {OP_NAME[op]}")
+
+
+def test_bad_env_value_throws():
+    os.environ["CCL_BF16"] = "avx9000"
+    with pytest.raises(_lib.MiReduceError):
+        comp.env_reload()
+
+
+def test_bf16_fp16_entry_points():
+    """ccl_bf16_reduce / ccl_fp16_reduce: the MPI user-op entries
+    (src/atl/mpi/atl_mpi_ctx.cpp:58-124)."""
+    s = _lib.shim()
+    b_impl, f_impl = impls()
+    n = 1000
+    for dt, fn in ((BF16, s.mi_ccl_bf16_reduce), (FP16, s.mi_ccl_fp16_reduce)):
+        a = rand_array(dt, n, seed=1)
+        b = rand_array(dt, n, seed=2)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, dt, 3, b_impl, f_impl)
+        oc = ctypes.c_size_t(0)
+        _lib.check_shim(fn(ptr(a), n, ptr(b), ctypes.byref(oc), 3))
+        assert oc.value == n
+        assert_same(b, exp, dt)
+    assert fn(ptr(a), n, ptr(b), None, 4) == -1  # custom -> CCL_FATAL in the reference
+
+
+@pytest.mark.parametrize("keep", [0, 1])
+@pytest.mark.parametrize("k", [1, 2, 5, 16, 23])
+@pytest.mark.parametrize("dt", [BF16, FP32, FP16])
+def test_comp_batch_reduce(keep, k, dt):
+    if keep and k > 16:
+        pytest.skip("keep-precision fan-in is bounded at 16 inputs")
+    if keep and dt != BF16:
+        pytest.skip("keep-precision mode reads bf16")
+    n = 4099
+    b_impl, f_impl = impls()
+    ins = [rand_array(dt, n, seed=300 + j) for j in range(k)]
+    packed = np.concatenate(ins)
+    offsets = [j * n for j in range(k)]
+    exp = ins[0].copy()
+    oc_ref = oracle.batch_reduce(packed, offsets, n, exp, dt, 0, keep, b_impl, f_impl)
+    got = ins[0].copy()
+    oc = comp.comp_batch_reduce(ptr(packed), offsets, n, ptr(got), comp.datatype(dt), comp.reduction.sum, keep)
+    assert_same(got, exp, dt)
+    assert oc == oc_ref
+
+
+def test_custom_reduction_callback():
+    """reduction::custom calls the user's fn on host memory (comp.cpp:84-88);
+    device operands are staged through the host (comp.cpp:136-195)."""
+    calls = []
+
+    def fn(in_p, count, inout_p, out_count_p, dtype, ctx):
+        calls.append((count, dtype))
+        src = np.ctypeslib.as_array(ctypes.cast(in_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst = np.ctypeslib.as_array(ctypes.cast(inout_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst[:] = dst * 2 + src
+
+    cb = _lib.MI_CCL_REDUCTION_FN(fn)
+    n = 1000
+    a = np.arange(n, dtype=np.float32)
+    b = np.ones(n, np.float32)
+    oc = ctypes.c_size_t(0)
+    _lib.check_shim(_lib.shim().mi_ccl_comp_reduce_custom(ptr(a), n, ptr(b), ctypes.byref(oc), FP32, cb))
+    assert np.array_equal(b, 2 + a)
+    ta, pa = to_dev(a)
+    tb, pb = to_dev(np.ones(n, np.float32))
+    _lib.check_shim(_lib.shim().mi_ccl_comp_reduce_custom(pa, n, pb, ctypes.byref(oc), FP32, cb))
+    assert np.array_equal(from_dev(tb, b), 2 + a)
+    assert calls == [(n, FP32), (n, FP32)]
+    null_fn = ctypes.cast(None, _lib.MI_CCL_REDUCTION_FN)
+    assert _lib.shim().mi_ccl_comp_reduce_custom(ptr(a), n, ptr(b), None, FP32, null_fn) == -1
+    assert b"callback" in _lib.shim().mi_ccl_last_error()
+
+
+@pytest.mark.parametrize("nt", [0, 1])
+def test_comp_copy(nt):
+    import torch
+    n = (5 << 20) + 3
+    src = np.random.default_rng(1).integers(0, 255, n, dtype=np.uint8)
+    dst = np.zeros_like(src)
+    comp.comp_copy(ptr(src), ptr(dst), n, bool(nt))
+    assert np.array_equal(src, dst)
+    td = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    comp.comp_copy(ptr(src), td.data_ptr(), n, bool(nt))
+    td2 = torch.zeros_like(td)
+    comp.comp_copy(td.data_ptr(), td2.data_ptr(), n - 16, bool(nt))
+    comp.comp_copy(td.data_ptr() + n - 16, td2.data_ptr() + n - 16, 16, bool(nt))
+    assert np.array_equal(td2.cpu().numpy(), src)
+    comp.comp_copy(0, 0, 0)  # bytes == 0 is success (comp.cpp:61-63)
+
+
+def test_concurrent_worker_threads():
+    """Up to CCL_WORKER_COUNT worker threads call ccl_comp_reduce at once
+    (src/exec/thread/worker.cpp:310-379): per-thread streams and scratch."""
+    b_impl, f_impl = impls()
+    n = 3_000_001
+    jobs = []
+    for t in range(6):
+        dt = [FP32, BF16, 4][t % 3]
+        a = rand_array(dt, n, seed=t)
+        b = rand_array(dt, n, seed=100 + t)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, dt, 0, b_impl, f_impl)
+        jobs.append((dt, a, b, exp))
+    errs = []
+
+    def work(job):
+        dt, a, b, _ = job
+        try:
+            comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype(dt), comp.reduction.sum)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(j,)) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    for dt, a, b, exp in jobs:
+        assert_same(b, exp, dt)
+
+
+FUNCTIONAL = [c for c in kat.load() if c["suite"] == "tests/functional"]
+
+
+@pytest.mark.parametrize("case", FUNCTIONAL, ids=[f"dt{c['dtype']}-{OP_NAME[c['op']]}-P{c['P']}-b{c['buf_idx']}"
+                                                  for c in FUNCTIONAL])
+def test_reference_functional_kats_through_dropin(case):
+    """oneCCL's tests/functional allreduce KATs with every local reduce done
+    by the drop-in ccl_comp_reduce on the GPU."""
+    dt = case["dtype"]
+    b_impl, _ = impls()
+
+    def reduce2(a, b):
+        comp.comp_reduce(ptr(a), a.size, ptr(b), comp.datatype(dt), comp.reduction(case["op"]))
+
+    for count in case["counts"]:
+        err, tol = kat.functional_case(case, count, reduce2, bf16_rne=(b_impl == 2))
+        assert err <= tol
+
+
+def test_reference_example_kats_through_dropin():
+    b_impl, _ = impls()
+    for c in kat.load():
+        if c["suite"] == "examples/cpu/cpu_allreduce_bf16_test":
+            assert kat.bf16_example_case(
+                c, lambda a, b: comp.comp_reduce(ptr(a), a.size, ptr(b), comp.datatype.bfloat16, comp.reduction.sum),
+                b_impl == 2)
+        elif c["suite"] == "examples/benchmark":
+            assert kat.benchmark_case(
+                c, lambda a, b: comp.comp_reduce(ptr(a), a.size, ptr(b), comp.datatype.float32, comp.reduction.sum))
