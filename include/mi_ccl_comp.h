@@ -45,6 +45,14 @@ int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_no
 int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
 /* ccl_fp16_reduce, src/comp/fp16/fp16.cpp:41-53 */
 int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
+/* ccl_convert_fp32_to_bf16_arrays / ccl_convert_bf16_to_fp32_arrays,
+ * src/comp/bf16/bf16.cpp:113-169 (rounding per the bf16 impl type) */
+int mi_ccl_convert_fp32_to_bf16_arrays(void* fp32_buf, void* bf16_buf, size_t count);
+int mi_ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t count);
+/* ccl_convert_fp32_to_fp16 / ccl_convert_fp16_to_fp32 (8 elements),
+ * src/comp/fp16/fp16.cpp:55-61 */
+int mi_ccl_convert_fp32_to_fp16(const void* src, void* dst);
+int mi_ccl_convert_fp16_to_fp32(const void* src, void* dst);
 /* ccl_reduction_to_str, src/comp/comp.cpp:251-260 */
 const char* mi_ccl_reduction_to_str(int op);
 /* Re-read CCL_BF16 / CCL_FP16 / CCL_COMP_HIP_DEVICE (env.cpp:711-720). */

@@ -144,6 +144,20 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal,
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal,
             void* stream);
 
+/* ---- precision conversions ------------------------------------------- *
+ * fp32 -> bf16 (MI_F_BF16_RNE: VCVTNEPS2BF16 semantics, else truncation;
+ * MI_F_BF16_TAIL_TRUNC16: the last count%16 elements truncate), fp32 -> fp16
+ * (RNE, VCVTPS2PH imm8=0), bf16 -> fp32 and fp16 -> fp32 (exact).  Replaces
+ * ccl_convert_fp32_to_bf16_arrays / ccl_convert_bf16_to_fp32_arrays
+ * (src/comp/bf16/bf16.cpp:113-169) and ccl_convert_fp32_to_fp16 /
+ * ccl_convert_fp16_to_fp32 (src/comp/fp16/fp16.cpp:55-61).
+ * mi_convert: device pointers, asynchronous.  mi_convert_sync: any pointer
+ * kinds, returns when dst is written.                                      */
+int mi_convert(const void* src, int src_dtype, void* dst, int dst_dtype,
+               size_t count, unsigned flags, void* stream);
+int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype,
+                    size_t count, unsigned flags, int device);
+
 /* ---- element-range sharding for 1..8 GPUs ------------- *
  * Contiguous [begin,end) of shard `rank` of `world`, boundaries rounded to
  * `align` elements (0 -> 256).  No data moves: each GPU reduces its shard of

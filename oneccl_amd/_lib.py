@@ -37,6 +37,8 @@ MI_API = [
     ("mi_reduce_multi", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_void_p]),
     ("mi_reduce_sync", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_uint, c_int]),
     ("mi_reduce_multi_sync", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int]),
+    ("mi_convert", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_void_p]),
+    ("mi_convert_sync", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_int]),
     ("mi_copy_sync", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int]),
     ("mi_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("mi_shard_range", c_int, [c_size_t, c_int, c_int, c_size_t, POINTER(c_size_t), POINTER(c_size_t)]),
@@ -60,6 +62,10 @@ SHIM_API = [
     ("mi_ccl_comp_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int]),
     ("mi_ccl_bf16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
     ("mi_ccl_fp16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
+    ("mi_ccl_convert_fp32_to_bf16_arrays", c_int, [c_void_p, c_void_p, c_size_t]),
+    ("mi_ccl_convert_bf16_to_fp32_arrays", c_int, [c_void_p, c_void_p, c_size_t]),
+    ("mi_ccl_convert_fp32_to_fp16", c_int, [c_void_p, c_void_p]),
+    ("mi_ccl_convert_fp16_to_fp32", c_int, [c_void_p, c_void_p]),
     ("mi_ccl_reduction_to_str", c_char_p, [c_int]),
     ("mi_ccl_env_reload", c_int, []),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),

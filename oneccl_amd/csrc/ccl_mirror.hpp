@@ -121,3 +121,9 @@ const char* ccl_reduction_to_str(ccl::reduction type);
 // src/comp/bf16/bf16.hpp:26-38, src/comp/fp16/fp16.hpp:21-35
 void ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op);
 void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op);
+void ccl_convert_fp32_to_bf16_arrays(void*, void*, size_t);
+void ccl_convert_bf16_to_fp32_arrays(void*, float*, size_t);
+void ccl_convert_fp32_to_bf16(const void* src, void* dst);  // 16 elements
+void ccl_convert_bf16_to_fp32(const void* src, void* dst);  // 16 elements
+void ccl_convert_fp32_to_fp16(const void* src, void* dst);  // 8 elements
+void ccl_convert_fp16_to_fp32(const void* src, void* dst);  // 8 elements

@@ -248,6 +248,43 @@ void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t*
           "mi_reduce_sync(fp16)");
 }
 
+// ---- conversions: bf16.cpp:113-169, fp16.cpp:55-61 ------------------------
+// ccl_convert_fp32_to_bf16_arrays: non-scalar impls convert (count/16)*16
+// elements with the impl's rounding (avx512bf RNE, avx512f truncate) and
+// truncate the tail; the scalar impl truncates all.
+static unsigned bf16_conv_flags() {
+    return mi_bf16_impl() == ccl_bf16_avx512bf ? (MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16) : 0u;
+}
+
+void ccl_convert_fp32_to_bf16_arrays(void* fp32_buf, void* bf16_buf, size_t count) {
+    check(mi_convert_sync(fp32_buf, MI_FLOAT32, bf16_buf, MI_BFLOAT16, count, bf16_conv_flags(), mi_comp_device()),
+          "mi_convert_sync(fp32->bf16)");
+}
+
+void ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t count) {
+    check(mi_convert_sync(bf16_buf, MI_BFLOAT16, fp32_buf, MI_FLOAT32, count, 0u, mi_comp_device()),
+          "mi_convert_sync(bf16->fp32)");
+}
+
+// 16-element forms (bf16.cpp:101-111): avx512bf -> RNE, otherwise truncate
+void ccl_convert_fp32_to_bf16(const void* src, void* dst) {
+    const unsigned f = mi_bf16_impl() == ccl_bf16_avx512bf ? MI_F_BF16_RNE : 0u;
+    check(mi_convert_sync(src, MI_FLOAT32, dst, MI_BFLOAT16, 16, f, mi_comp_device()), "mi_convert_sync");
+}
+
+void ccl_convert_bf16_to_fp32(const void* src, void* dst) {
+    check(mi_convert_sync(src, MI_BFLOAT16, dst, MI_FLOAT32, 16, 0u, mi_comp_device()), "mi_convert_sync");
+}
+
+// 8-element forms (fp16.cpp:55-61): VCVTPS2PH RNE / VCVTPH2PS
+void ccl_convert_fp32_to_fp16(const void* src, void* dst) {
+    check(mi_convert_sync(src, MI_FLOAT32, dst, MI_FLOAT16, 8, 0u, mi_comp_device()), "mi_convert_sync");
+}
+
+void ccl_convert_fp16_to_fp32(const void* src, void* dst) {
+    check(mi_convert_sync(src, MI_FLOAT16, dst, MI_FLOAT32, 8, 0u, mi_comp_device()), "mi_convert_sync");
+}
+
 // ccl_comp_reduce_regular, comp.cpp:76-121
 static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
                                        const ccl_datatype& dtype, ccl::reduction reduction,
@@ -393,6 +430,34 @@ int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_
 int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
     MI_SHIM_GUARD({
         ccl_fp16_reduce(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
+        return 0;
+    });
+}
+
+int mi_ccl_convert_fp32_to_bf16_arrays(void* fp32_buf, void* bf16_buf, size_t count) {
+    MI_SHIM_GUARD({
+        ccl_convert_fp32_to_bf16_arrays(fp32_buf, bf16_buf, count);
+        return 0;
+    });
+}
+
+int mi_ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t count) {
+    MI_SHIM_GUARD({
+        ccl_convert_bf16_to_fp32_arrays(bf16_buf, fp32_buf, count);
+        return 0;
+    });
+}
+
+int mi_ccl_convert_fp32_to_fp16(const void* src, void* dst) {
+    MI_SHIM_GUARD({
+        ccl_convert_fp32_to_fp16(src, dst);
+        return 0;
+    });
+}
+
+int mi_ccl_convert_fp16_to_fp32(const void* src, void* dst) {
+    MI_SHIM_GUARD({
+        ccl_convert_fp16_to_fp32(src, dst);
         return 0;
     });
 }

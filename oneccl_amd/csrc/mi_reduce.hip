@@ -399,6 +399,52 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// conversions
+// ---------------------------------------------------------------------------
+typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&);
+
+template <typename ST, typename DT, unsigned V>
+hipError_t conv_one(dim3 grid, hipStream_t s, const CArgs& a) {
+    hipLaunchKernelGGL((convert_kernel<ST, DT, V>), grid, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+ConvFn pick_conv(int sdt, int ddt, unsigned f) {
+    if (sdt == MI_FLOAT32 && ddt == MI_BFLOAT16) {
+        if (!(f & V_BF16_RNE)) return &conv_one<float, bf16_tag, 0u>;
+        return (f & V_TAIL_TRUNC) ? &conv_one<float, bf16_tag, V_BF16_RNE | V_TAIL_TRUNC>
+                                  : &conv_one<float, bf16_tag, V_BF16_RNE>;
+    }
+    if (sdt == MI_FLOAT32 && ddt == MI_FLOAT16) return &conv_one<float, fp16_tag, 0u>;
+    if (sdt == MI_BFLOAT16 && ddt == MI_FLOAT32) return &conv_one<bf16_tag, float, 0u>;
+    if (sdt == MI_FLOAT16 && ddt == MI_FLOAT32) return &conv_one<fp16_tag, float, 0u>;
+    return nullptr;
+}
+
+int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, unsigned flags, hipStream_t s,
+                   uint64_t trunc_from) {
+    ConvFn fn = pick_conv(sdt, ddt, flags);
+    if (!fn) return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
+    if (count == 0) return 0;
+    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    CArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = src;
+    a.dst = dst;
+    a.count = count;
+    a.trunc_from = trunc_from;
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src), da = reinterpret_cast<uintptr_t>(dst);
+    a.scalar_only = ((sa | da) & 15u) ? 1 : 0;  // vector path: 16-byte aligned src and dst
+    a.ngroups = a.scalar_only ? 0 : count / 8;
+    const uint64_t work = a.scalar_only ? count : std::max<uint64_t>(a.ngroups, 1);
+    uint64_t blocks = std::min<uint64_t>((work + kBlock - 1) / kBlock, 1u << 20);
+    blocks = std::max<uint64_t>(blocks, 1);
+    hipError_t e = fn(dim3((unsigned)blocks), s, a);
+    if (e != hipSuccess) return hip_fail(e, "convert kernel launch");
+    return 0;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -434,6 +480,68 @@ int mi_reduce_multi_sync(const void* const* inputs, int k, void* out, size_t cou
                          int op, unsigned flags, int device) {
     if (!inputs) return fail(MI_E_INVALID, "null input list");
     return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+}
+
+int mi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags,
+               void* stream) {
+    return launch_convert(src, src_dtype, dst, dst_dtype, count, flags, (hipStream_t)stream, (count / 16) * 16);
+}
+
+int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags,
+                    int device) {
+    if (!pick_conv(src_dtype, dst_dtype, flags))
+        return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
+    if (count == 0) return 0;
+    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    int pdev = -1;
+    const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+    if (device < 0 && pdev >= 0) device = pdev;
+    DevCtx* d = nullptr;
+    int rc = get_ctx(device, &d);
+    if (rc) return rc;
+    int prev = 0;
+    MI_HIP(hipGetDevice(&prev));
+    if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+    struct Restore {
+        int dev, cur;
+        ~Restore() {
+            if (dev != cur) (void)hipSetDevice(dev);
+        }
+    } restore{prev, d->device};
+    const uint64_t trunc_from = (count / 16) * 16;
+    if (ks == PK_DEVICE && kd == PK_DEVICE) {
+        rc = launch_convert(src, src_dtype, dst, dst_dtype, count, flags, d->stream[0], trunc_from);
+        if (rc) return rc;
+        MI_HIP(hipStreamSynchronize(d->stream[0]));
+        return 0;
+    }
+    const size_t ss = dtype_size(src_dtype), ds = dtype_size(dst_dtype);
+    size_t chunk = kChunkBytes / std::max(ss, ds);
+    chunk -= chunk % 16;
+    rc = ensure_scratch(d, 2, chunk * std::max(ss, ds));
+    if (rc) return rc;
+    for (size_t off = 0, c = 0; off < count; off += chunk, c++) {
+        const int sl = (int)(c & 1);
+        hipStream_t st = d->stream[sl];
+        const size_t n = std::min(chunk, count - off);
+        const void* sp = static_cast<const char*>(src) + off * ss;
+        void* dp = static_cast<char*>(dst) + off * ds;
+        const void* dsrc = sp;
+        void* ddst = dp;
+        if (ks != PK_DEVICE) {
+            MI_HIP(hipMemcpyAsync(d->dbuf[sl][0], sp, n * ss, hipMemcpyHostToDevice, st));
+            dsrc = d->dbuf[sl][0];
+        }
+        if (kd != PK_DEVICE) ddst = d->dbuf[sl][1];
+        // chunk starts are multiples of 16: the tail split is the global one
+        rc = launch_convert(dsrc, src_dtype, ddst, dst_dtype, n, flags, st,
+                            trunc_from > off ? std::min<uint64_t>(trunc_from - off, n) : 0);
+        if (rc) return rc;
+        if (kd != PK_DEVICE) MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
+    }
+    MI_HIP(hipStreamSynchronize(d->stream[0]));
+    MI_HIP(hipStreamSynchronize(d->stream[1]));
+    return 0;
 }
 
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {

@@ -48,6 +48,18 @@ void add_reduce(std::vector<Variant>& vs, KArgs a, int cap, double traffic) {
                   }, {}});
 }
 
+template <int KT, int U>
+void add_fanin(std::vector<Variant>& vs, KArgs a, double traffic) {
+    const uint64_t tile = (uint64_t)kBlock * U;
+    const uint64_t blocks = (a.nvec + tile - 1) / tile;
+    char name[128];
+    snprintf(name, sizeof name, "fanin8 KT=%d U=%d mem=3 grid=%llu", KT, U, (unsigned long long)blocks);
+    vs.push_back({name, traffic, [a, blocks](hipStream_t s) {
+                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, KT, U, 3>), dim3((unsigned)blocks),
+                                         dim3(kBlock), 0, s, a);
+                  }, {}});
+}
+
 int main(int argc, char** argv) {
     const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
@@ -74,16 +86,36 @@ int main(int argc, char** argv) {
     const double t3 = 3.0 * bytes;
 
     std::vector<Variant> vs;
-    const int caps[] = {0, 256, 512, 1024, 2048, 4096, 8192};
+    const int caps[] = {0, 512, 2048};
     for (int cap : caps) {
-        add_reduce<1, 2>(vs, a, cap, t3);
-        add_reduce<2, 2>(vs, a, cap, t3);
-        add_reduce<4, 0>(vs, a, cap, t3);
-        add_reduce<4, 1>(vs, a, cap, t3);
+        add_reduce<1, 3>(vs, a, cap, t3);
+        add_reduce<2, 3>(vs, a, cap, t3);
         add_reduce<4, 2>(vs, a, cap, t3);
         add_reduce<4, 3>(vs, a, cap, t3);
-        add_reduce<8, 2>(vs, a, cap, t3);
+        add_reduce<8, 3>(vs, a, cap, t3);
     }
+    // 8-input fan-in (C4): 7 more input buffers, one output
+    std::vector<float*> fan(8, nullptr);
+    fan[0] = io;
+    fan[1] = in;
+    for (int j = 2; j < 8; j++) {
+        CK(hipMalloc(&fan[j], bytes));
+        CK(hipMemset(fan[j], 0x3c, bytes));
+    }
+    KArgs f8{};
+    for (int j = 0; j < 8; j++) f8.in[j] = fan[j];
+    f8.out = cp;
+    f8.k = 8;
+    f8.count = n;
+    f8.nvec = n / 4;
+    f8.trunc_from = n;
+    const double t9 = 9.0 * bytes;
+    add_fanin<0, 4>(vs, f8, t9);
+    add_fanin<8, 1>(vs, f8, t9);
+    add_fanin<8, 2>(vs, f8, t9);
+    add_fanin<8, 4>(vs, f8, t9);
+    add_fanin<0, 2>(vs, f8, t9);
+    add_fanin<0, 1>(vs, f8, t9);
     vs.push_back({"hipMemcpyAsync D2D", 2.0 * bytes,
                   [=](hipStream_t st) { (void)hipMemcpyAsync(cp, in, bytes, hipMemcpyDeviceToDevice, st); }, {}});
     for (int mem : {0, 2}) {
