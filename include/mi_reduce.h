@@ -81,7 +81,7 @@ enum mi_dtype {
 #define MI_F_ACC_FP32 0x4u
 /* With MI_F_ACC_FP32|MI_F_BF16_RNE: the last (count % 16) elements of the
  * final fp32 -> bf16 conversion are truncated, as the scalar tail loop of
- * ccl_convert_fp32_to_bf16_arrays does (src/comp/bf16/bf16.cpp:132-143).   */
+ * ccl_convert_fp32_to_bf16_arrays does (src/comp/bf16/bf16.cpp:145-148).   */
 #define MI_F_BF16_TAIL_TRUNC16 0x8u
 
 /* Error codes (< 0). */

@@ -8,7 +8,7 @@
 //   ccl_reduction_to_str    src/comp/comp.cpp:251-260
 //   ccl_bf16_reduce         src/comp/bf16/bf16.cpp:87-110
 //   ccl_fp16_reduce         src/comp/fp16/fp16.cpp:41-53
-//   bf16_impl_names / fp16_impl_names / fp16_env_impl_names (bf16.cpp:29-33, fp16.cpp:29-41)
+//   bf16_impl_names / fp16_impl_names / fp16_env_impl_names (bf16.cpp:26-30, fp16.cpp:25-39)
 // Which bit-level behaviour the reference would show (bf16 truncation vs
 // RNE, min/max operand order) is taken from the same place the reference
 // takes it: the bf16/fp16 impl type chosen from CPUID and CCL_BF16/CCL_FP16
@@ -44,7 +44,7 @@ static int mi_comp_device() { return -1; }
 #define MI_CCL_THROW(msg) throw ccl::exception(msg)
 #endif
 
-// bf16.cpp:29-33, fp16.cpp:29-41 — referenced by env.cpp:711-720, 1101-1102
+// bf16.cpp:26-30, fp16.cpp:25-39 — referenced by env.cpp:711-720, 1101-1102
 std::map<ccl_bf16_impl_type, std::string> bf16_impl_names = {
     std::make_pair(ccl_bf16_scalar, "scalar"), std::make_pair(ccl_bf16_avx512f, "avx512f"),
     std::make_pair(ccl_bf16_avx512bf, "avx512bf")};
@@ -266,7 +266,7 @@ void ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t cou
           "mi_convert_sync(bf16->fp32)");
 }
 
-// 16-element forms (bf16.cpp:101-111): avx512bf -> RNE, otherwise truncate
+// 16-element forms (bf16.cpp:113-128): avx512bf -> RNE, otherwise truncate
 void ccl_convert_fp32_to_bf16(const void* src, void* dst) {
     const unsigned f = mi_bf16_impl() == ccl_bf16_avx512bf ? MI_F_BF16_RNE : 0u;
     check(mi_convert_sync(src, MI_FLOAT32, dst, MI_BFLOAT16, 16, f, mi_comp_device()), "mi_convert_sync");
@@ -335,7 +335,7 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
         for (size_t i = 1; i < k; i++) ins[i] = static_cast<const char*>(in_buf) + es * offsets[i];
         // acc uses CCL_REDUCE(float) order (std::min/max); final conversion
         // per impl: avx512bf RNE on (count/16)*16 elements + truncated tail,
-        // avx512f / scalar truncate all (bf16.cpp:113-143)
+        // avx512f / scalar truncate all (bf16.cpp:130-149)
         unsigned f = MI_F_ACC_FP32;
         if (mi_bf16_impl() == ccl_bf16_avx512bf) f |= MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16;
         check(mi_reduce_multi_sync(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16,

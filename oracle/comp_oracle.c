@@ -308,8 +308,8 @@ int orc_comp_reduce_mt(const void* in_buf, size_t n, void* inout_buf, int dtype,
 /* array conversions, src/comp/bf16/bf16.cpp:113-169                    */
 /* ------------------------------------------------------------------ */
 /* Non-scalar impls convert the first (count/16)*16 elements 16 at a time
- * (avx512bf -> RNE, avx512f -> truncate, bf16.cpp:117-130) and the remaining
- * tail with the scalar truncation (:132-143).  Scalar impl: all truncated. */
+ * (avx512bf -> RNE, avx512f -> truncate, bf16.cpp:136-143) and the remaining
+ * tail with the scalar truncation (:145-148).  Scalar impl: all truncated. */
 void orc_convert_fp32_to_bf16_arrays(const float* src, uint16_t* dst, size_t count,
                                      int bf16_impl) {
     size_t limit = 0, i;

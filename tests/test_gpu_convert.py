@@ -71,7 +71,7 @@ def test_lp_to_fp32_all_patterns(sdt):
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 4099, 1 << 20])
 @pytest.mark.parametrize("impl", [0, 1, 2])
 def test_fp32_to_bf16_arrays_tail_semantics(n, impl):
-    """ccl_convert_fp32_to_bf16_arrays (bf16.cpp:113-143): avx512bf rounds the
+    """ccl_convert_fp32_to_bf16_arrays (bf16.cpp:130-149): avx512bf rounds the
     first (count/16)*16 elements and truncates the tail."""
     rng = np.random.default_rng(n)
     src = (rng.standard_normal(n) * 3).astype(np.float32)
