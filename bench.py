@@ -284,8 +284,9 @@ def host_resident_leg(m, dt, es, op, flags, n):
     import torch
     res = {}
     nbytes = n * es
-    for kind in ("pinned", "pageable"):
-        if kind == "pinned":
+    for kind in ("pinned", "pinned_staged", "pageable"):
+        m.mi_set_host_mode(1 if kind == "pinned_staged" else 0)
+        if kind.startswith("pinned"):
             a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
             b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
             pa, pb = a.data_ptr(), b.data_ptr()
@@ -302,8 +303,11 @@ def host_resident_leg(m, dt, es, op, flags, n):
             if rc:
                 return {"error": m.mi_last_error().decode()}
         res[kind] = round(nbytes / GiB / min(times), 3)
-    return {"unit": "GiB/s bucket incl. H2D of both operands and D2H of the result",
-            "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync"}
+    m.mi_set_host_mode(0)
+    return {"unit": "GiB/s bucket incl. both operands host->GPU and the result GPU->host over PCIe",
+            "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync",
+            "modes": "pinned = zero-copy kernel on pinned host memory (default); pinned_staged = chunked "
+                     "H2D/kernel/D2H over two streams; pageable = staged"}
 
 
 def pmc_traffic(config):

@@ -171,6 +171,17 @@ int mi_shard_range(size_t count, int rank, int world, size_t align,
  * sycl::get_pointer_type for (src/comp/comp.cpp:145-147).                 */
 int mi_pointer_kind(const void* ptr, int* device);
 
+/* ---- host-operand strategy ------------------------------------------- *
+ * How mi_*_sync treats host operands.  MI_HOST_AUTO (default): pinned host
+ * memory is read and written in place by the kernel over PCIe (zero-copy,
+ * full duplex), pageable memory is staged; MI_HOST_STAGED: always stage
+ * (chunked H2D -> kernel -> D2H on two streams); MI_HOST_ZEROCOPY: as AUTO.
+ * Env: MI_REDUCE_HOST_MODE=auto|staged.  Returns the previous mode.       */
+#define MI_HOST_AUTO 0
+#define MI_HOST_STAGED 1
+#define MI_HOST_ZEROCOPY 2
+int mi_set_host_mode(int mode);
+
 /* ---- introspection ---------------------------------------------------- */
 
 /* ccl_reduction_to_str, src/comp/comp.cpp:251-260. */

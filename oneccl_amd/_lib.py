@@ -50,6 +50,7 @@ MI_API = [
     ("mi_device_count", c_int, []),
     ("mi_get_launch_config", c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     ("mi_set_max_blocks", c_int, [c_int]),
+    ("mi_set_host_mode", c_int, [c_int]),
 ]
 
 # mirrors include/mi_ccl_comp.h

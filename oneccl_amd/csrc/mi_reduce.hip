@@ -47,6 +47,17 @@ constexpr int kUnroll = 4;  // 16-byte vectors per lane per input per tile
 constexpr int kMem = 3;     // non-temporal loads and stores (sweep: profiles/round1_sweep.jsonl)
 
 std::atomic<int> g_max_blocks{-1};  // -1 = not yet read from env; 0 = no cap
+std::atomic<int> g_host_mode{-1};   // -1 = not yet read from env
+
+int host_mode() {
+    int v = g_host_mode.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* s = getenv("MI_REDUCE_HOST_MODE");
+        v = (s && strcmp(s, "staged") == 0) ? MI_HOST_STAGED : MI_HOST_AUTO;
+        g_host_mode.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
 
 int max_blocks() {
     int v = g_max_blocks.load(std::memory_order_relaxed);
@@ -280,7 +291,8 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
 
 enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
 
-PtrKind classify(const void* p, int* dev) {
+// `devptr` (optional): the device-visible address of a pinned host pointer.
+PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
@@ -292,7 +304,10 @@ PtrKind classify(const void* p, int* dev) {
         *dev = at.device;
         return PK_DEVICE;
     }
-    if (at.type == hipMemoryTypeHost) return PK_PINNED;
+    if (at.type == hipMemoryTypeHost) {
+        if (devptr) *devptr = at.devicePointer ? at.devicePointer : const_cast<void*>(p);
+        return PK_PINNED;
+    }
     return PK_PAGEABLE;
 }
 
@@ -310,13 +325,17 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
         if (!inputs[i]) return fail(MI_E_INVALID, "null input");
 
     PtrKind kin[MI_MAX_INPUTS];
+    const void* dins[MI_MAX_INPUTS];
     int pdev = -1;
     bool all_dev = true;
     for (int i = 0; i < k; i++) {
-        kin[i] = classify(inputs[i], &pdev);
+        void* dp = const_cast<void*>(inputs[i]);
+        kin[i] = classify(inputs[i], &pdev, &dp);
+        dins[i] = dp;
         all_dev = all_dev && kin[i] == PK_DEVICE;
     }
-    const PtrKind kout = classify(out, &pdev);
+    void* dout = out;
+    const PtrKind kout = classify(out, &pdev, &dout);
     all_dev = all_dev && kout == PK_DEVICE;
     if (device < 0 && pdev >= 0) device = pdev;
 
@@ -333,8 +352,14 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
         }
     } restore{prev, d->device};
 
-    if (all_dev) {
-        rc = launch_reduce(inputs, k, out, count, dt, op, flags, d->stream[0]);
+    // zero-copy: pinned host operands are read/written by the kernel in place
+    // over PCIe (both directions at once); device operands as they are
+    bool direct = true;
+    for (int i = 0; i < k; i++) direct = direct && (kin[i] == PK_DEVICE || kin[i] == PK_PINNED);
+    direct = direct && (kout == PK_DEVICE || kout == PK_PINNED);
+    if (!all_dev && direct && host_mode() == MI_HOST_STAGED) direct = false;
+    if (all_dev || direct) {
+        rc = launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
         if (rc) return rc;
         MI_HIP(hipStreamSynchronize(d->stream[0]));
         return 0;
@@ -638,6 +663,13 @@ int mi_device_count(void) {
         return 0;
     }
     return n;
+}
+
+int mi_set_host_mode(int mode) {
+    if (mode < MI_HOST_AUTO || mode > MI_HOST_ZEROCOPY) return fail(MI_E_INVALID, "bad host mode");
+    const int prev = host_mode();
+    g_host_mode.store(mode == MI_HOST_ZEROCOPY ? MI_HOST_AUTO : mode, std::memory_order_relaxed);
+    return prev;
 }
 
 int mi_get_launch_config(int* block, int* unroll, int* max_blocks_out) {

@@ -43,6 +43,7 @@ def lib() -> ctypes.CDLL:
                                             POINTER(c_float), c_int, c_int]
         L.orc_convert_fp32_to_bf16_arrays.argtypes = [c_void_p, c_void_p, c_size_t, c_int]
         L.orc_convert_bf16_to_fp32_arrays.argtypes = [c_void_p, c_void_p, c_size_t]
+        L.orc_convert_fp32_to_fp16_arrays.argtypes = [c_void_p, c_void_p, c_size_t]
         L.orc_bf16_to_fp32.argtypes = [c_uint16]
         L.orc_bf16_to_fp32.restype = c_float
         L.orc_fp32_to_bf16_trunc.argtypes = [c_float]
@@ -139,9 +140,11 @@ def bf16_to_f32(b: np.ndarray) -> np.ndarray:
 
 
 def f32_to_fp16(x: np.ndarray) -> np.ndarray:
-    """numpy's float16 cast is IEEE RNE; equals VCVTPS2PH imm8=0 except NaN
-    payloads (checked in tests/test_oracle.py)."""
-    return np.asarray(x, np.float32).astype(np.float16).view(np.uint16)
+    """VCVTPS2PH imm8=0 over an array (the oracle's scalar restatement, in C)."""
+    src = np.ascontiguousarray(x, np.float32)
+    out = np.empty(src.shape, np.uint16)
+    lib().orc_convert_fp32_to_fp16_arrays(src.ctypes.data, out.ctypes.data, src.size)
+    return out
 
 
 def fp16_to_f32(h: np.ndarray) -> np.ndarray:

@@ -322,6 +322,12 @@ void orc_convert_fp32_to_bf16_arrays(const float* src, uint16_t* dst, size_t cou
     for (i = limit; i < count; i++) dst[i] = orc_fp32_to_bf16_trunc(src[i]);
 }
 
+/* ccl_convert_fp32_to_fp16 (fp16.cpp:55-57) applied over an array: VCVTPS2PH
+ * imm8 = 0 on every element. */
+void orc_convert_fp32_to_fp16_arrays(const float* src, uint16_t* dst, size_t count) {
+    for (size_t i = 0; i < count; i++) dst[i] = orc_fp32_to_fp16_rne(src[i]);
+}
+
 void orc_convert_bf16_to_fp32_arrays(const uint16_t* src, float* dst, size_t count) {
     for (size_t i = 0; i < count; i++) dst[i] = orc_bf16_to_fp32(src[i]);
 }

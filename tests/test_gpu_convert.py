@@ -42,7 +42,7 @@ def test_fp32_to_lp_all_bit_patterns(ddt, flags):
     dev_out = torch.empty(CHUNK, dtype=torch.int16, device="cuda")
     exp = np.empty(CHUNK, np.uint16)
     for c in range((1 << 32) // CHUNK):
-        host = np.arange(c * CHUNK, (c + 1) * CHUNK, dtype=np.uint64).astype(np.uint32)
+        host = np.arange(CHUNK, dtype=np.uint32) + np.uint32(c * CHUNK)
         dev_in = torch.arange(c * CHUNK, (c + 1) * CHUNK, dtype=torch.int64, device="cuda").to(torch.int32)
         _lib.check(m.mi_convert(dev_in.data_ptr(), FP32, dev_out.data_ptr(), ddt, CHUNK, flags, _stream()))
         if ddt == BF16:

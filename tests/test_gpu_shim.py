@@ -87,6 +87,29 @@ def test_comp_reduce_pointer_kinds(where, dt):
     assert_same(got, exp, dt, where)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["zero_copy", "staged"])
+@pytest.mark.parametrize("dt", [FP32, BF16, 4])
+def test_pinned_host_modes(mode, dt):
+    """Pinned host operands: zero-copy kernel over PCIe (default) or the staged
+    H2D / kernel / D2H pipeline — same bits."""
+    import torch
+    n = (40 << 20) // 4 + 77
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=61, specials=False)
+    b = rand_array(dt, n, seed=62, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+    ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+    hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+    m = _lib.mi()
+    prev = m.mi_set_host_mode(mode)
+    try:
+        comp.comp_reduce(ha.data_ptr() + 0, n, hb.data_ptr(), comp.datatype(dt), comp.reduction.sum)
+    finally:
+        m.mi_set_host_mode(prev)
+    assert_same(hb.numpy().view(b.dtype), exp, dt)
+
+
 @pytest.mark.parametrize("dt", [FP32, BF16])
 def test_large_host_buffer_pipelined(dt):
     """> 1 staging chunk (32 MiB): the H2D / kernel / D2H pipeline over two

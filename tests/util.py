@@ -79,14 +79,14 @@ def is_nan_bits(a: np.ndarray, dtype: int) -> np.ndarray:
 
 def assert_same(got: np.ndarray, exp: np.ndarray, dtype: int, what: str = "") -> None:
     """Bit-exact, NaN-payload-agnostic comparison."""
-    assert got.shape == exp.shape
-    gb = got.view(np.uint8).reshape(got.size, -1)
-    eb = exp.view(np.uint8).reshape(exp.size, -1)
-    diff = np.any(gb != eb, axis=1)
-    nn = is_nan_bits(got, dtype) & is_nan_bits(exp, dtype)
-    bad = diff & ~nn
-    if bad.any():
-        i = np.flatnonzero(bad)
+    assert got.shape == exp.shape and got.itemsize == exp.itemsize
+    iv = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[got.itemsize]
+    cand = np.flatnonzero(got.view(iv) != exp.view(iv))
+    if cand.size:
+        both_nan = is_nan_bits(got[cand], dtype) & is_nan_bits(exp[cand], dtype)
+        cand = cand[~both_nan]
+    if cand.size:
+        i = cand
         raise AssertionError(f"{what}: {len(i)} of {got.size} elements differ; first at {i[:5].tolist()}: "
                              f"got {got[i[:5]].tolist()} expected {exp[i[:5]].tolist()}")
 

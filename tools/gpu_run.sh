@@ -37,6 +37,8 @@ for step in "$@"; do
             run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
             run bench 600 python bench.py ;;
+        sizes)
+            run sizes 600 python tools/size_sweep.py ;;
         benchall)
             for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
