@@ -37,6 +37,9 @@ for step in "$@"; do
             run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
             run bench 600 python bench.py ;;
+        c1)
+            run c1_dropin 300 python tools/c1_allreduce.py --reduce dropin &&
+            run c1_oracle 300 python tools/c1_allreduce.py --reduce oracle ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
         benchall)
