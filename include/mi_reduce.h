@@ -134,6 +134,31 @@ int mi_reduce_multi_sync(const void* const* inputs, int k, void* out,
                          size_t count, int dtype, int op, unsigned flags,
                          int device);
 
+/* ---- asynchronous form of the pointer-kind-agnostic entry ------------ *
+ * Issues the same work as mi_reduce_multi_sync and returns at once with a
+ * request; mi_test polls it (done = 1 when inputs may be reused and `out` is
+ * final), mi_wait blocks, mi_request_free releases it (after completion).
+ * Lets a schedule entry return `started` and poll from update() instead of
+ * blocking its worker thread (reduce_local_entry.cpp:
+ * 116-135 polls the Level Zero path the same way).  Pageable host operands
+ * are staged by copies that may block inside mi_reduce_start.            */
+typedef struct mi_request* mi_request_t;
+int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count,
+                    int dtype, int op, unsigned flags, int device,
+                    mi_request_t* req);
+int mi_test(mi_request_t req, int* done);
+int mi_wait(mi_request_t req);
+int mi_request_free(mi_request_t req);
+
+/* ---- in-process multi-GPU element-range shards --------- *
+ * Shard s folds inputs[s*k .. s*k+k-1] into outs[s] (counts[s] elements) on
+ * HIP device devices[s] — all pointers of a shard live on its device.  Every
+ * shard is launched before any is waited for; no inter-GPU traffic, no
+ * collective.  Synchronous.                                                */
+int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs,
+                      int k, void* const* outs, const size_t* counts, int dtype,
+                      int op, unsigned flags);
+
 /* Byte copy, synchronous, any pointer kinds.  Replaces the body of
  * ccl_comp_copy, src/comp/comp.cpp:60-74 (nontemporal flag honoured on the
  * device path by non-temporal stores).                                     */

@@ -39,6 +39,13 @@ MI_API = [
     ("mi_reduce_multi_sync", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int]),
     ("mi_convert", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_void_p]),
     ("mi_convert_sync", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_int]),
+    ("mi_reduce_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
+                                POINTER(c_void_p)]),
+    ("mi_test", c_int, [c_void_p, POINTER(c_int)]),
+    ("mi_wait", c_int, [c_void_p]),
+    ("mi_request_free", c_int, [c_void_p]),
+    ("mi_reduce_sharded", c_int, [c_int, POINTER(c_int), POINTER(c_void_p), c_int, POINTER(c_void_p),
+                                  POINTER(c_size_t), c_int, c_int, c_uint]),
     ("mi_copy_sync", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int]),
     ("mi_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("mi_shard_range", c_int, [c_size_t, c_int, c_int, c_size_t, POINTER(c_size_t), POINTER(c_size_t)]),

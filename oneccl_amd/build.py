@@ -73,6 +73,18 @@ def build_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_dropin_caller(force: bool = False) -> Path:
+    """Test program: a C++ caller linking libccl_comp_hip.so by oneCCL's own
+    mangled names (tests/cpp/dropin_caller.cpp)."""
+    src = ROOT / "tests" / "cpp" / "dropin_caller.cpp"
+    out = ROOT / "tests" / "cpp" / "dropin_caller"
+    deps = [src, CSRC / "ccl_mirror.hpp", LIB / "libccl_comp_hip.so"]
+    if src.exists() and (force or _stale(out, deps)):
+        _run([_hipcc(), "-O2", "-std=c++17", "-o", str(out), str(src), f"-L{LIB}", "-lccl_comp_hip",
+              "-lmi_reduce", f"-Wl,-rpath,{LIB}", "-Wl,-rpath,$ORIGIN/../../oneccl_amd/lib"])
+    return out
+
+
 def build_oracle(force: bool = False) -> Path:
     """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile)."""
     odir = ROOT / "oracle"
@@ -86,6 +98,7 @@ def build_all(force: bool = False) -> None:
     build_mi_reduce(force)
     build_shim(force)
     build_sweep(force)
+    build_dropin_caller(force)
     build_oracle(force)
 
 

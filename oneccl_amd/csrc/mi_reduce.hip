@@ -311,11 +311,15 @@ PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
     return PK_PAGEABLE;
 }
 
-// Synchronous fold with any pointer kinds.  All-device: one launch + stream
-// sync.  Otherwise: chunks of kChunkBytes, two pipeline slots on two
-// streams (H2D of chunk c+1 overlaps the kernel / D2H of chunk c).
-int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
-                unsigned flags, int device) {
+// Issue a fold with any pointer kinds on the calling thread's streams of the
+// chosen device; *used = the streams that carry work (bit 0: stream[0],
+// bit 1: stream[1]).  All-device or zero-copy: one launch on stream[0].
+// Otherwise: chunks of kChunkBytes, two pipeline slots on two streams (H2D
+// of chunk c+1 overlaps the kernel / D2H of chunk c).
+int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
+                 unsigned flags, int device, DevCtx** ctx, int* used) {
+    *ctx = nullptr;
+    *used = 0;
     const size_t es = dtype_size(dt);
     if (!es) return fail(MI_E_INVALID, "unknown datatype");
     if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
@@ -342,6 +346,7 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     DevCtx* d = nullptr;
     int rc = get_ctx(device, &d);
     if (rc) return rc;
+    *ctx = d;
     int prev = 0;
     MI_HIP(hipGetDevice(&prev));
     if (prev != d->device) MI_HIP(hipSetDevice(d->device));
@@ -359,10 +364,8 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     direct = direct && (kout == PK_DEVICE || kout == PK_PINNED);
     if (!all_dev && direct && host_mode() == MI_HOST_STAGED) direct = false;
     if (all_dev || direct) {
-        rc = launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
-        if (rc) return rc;
-        MI_HIP(hipStreamSynchronize(d->stream[0]));
-        return 0;
+        *used = 1;
+        return launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
     }
 
     // distinct host operands get a device staging buffer per slot; `out`
@@ -388,6 +391,7 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     if (rc) return rc;
 
     const size_t nchunks = (count + chunk_elems - 1) / chunk_elems;
+    *used = nchunks > 1 ? 3 : 1;
     for (size_t c = 0; c < nchunks; c++) {
         const int s = (int)(c & 1);
         hipStream_t st = d->stream[s];
@@ -419,8 +423,17 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
         if (slot_of[k] >= 0)
             MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, dout, bytes, hipMemcpyDeviceToHost, st));
     }
-    MI_HIP(hipStreamSynchronize(d->stream[0]));
-    MI_HIP(hipStreamSynchronize(d->stream[1]));
+    return 0;
+}
+
+int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
+                unsigned flags, int device) {
+    DevCtx* d = nullptr;
+    int used = 0;
+    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used);
+    if (rc) return rc;
+    for (int s = 0; s < 2; s++)
+        if (used & (1 << s)) MI_HIP(hipStreamSynchronize(d->stream[s]));
     return 0;
 }
 
@@ -567,6 +580,104 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
     MI_HIP(hipStreamSynchronize(d->stream[0]));
     MI_HIP(hipStreamSynchronize(d->stream[1]));
     return 0;
+}
+
+// ---- asynchronous requests ------------------------------------------------
+struct mi_request {
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int nev = 0;
+    int device = -1;
+};
+
+int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                    unsigned flags, int device, mi_request_t* req) {
+    if (!req) return fail(MI_E_INVALID, "null request pointer");
+    *req = nullptr;
+    if (!inputs) return fail(MI_E_INVALID, "null input list");
+    DevCtx* d = nullptr;
+    int used = 0;
+    int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used);
+    if (rc) return rc;
+    mi_request* r = new mi_request();
+    if (d) {
+        r->device = d->device;
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+        for (int s = 0; s < 2 && rc == 0; s++) {
+            if (!(used & (1 << s))) continue;
+            hipError_t e = hipEventCreateWithFlags(&r->ev[r->nev], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(r->ev[r->nev], d->stream[s]);
+            if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+            r->nev++;
+        }
+        if (prev != d->device) (void)hipSetDevice(prev);
+    }
+    if (rc) {
+        mi_request_free(r);
+        return rc;
+    }
+    *req = r;
+    return 0;
+}
+
+int mi_test(mi_request_t req, int* done) {
+    if (!req || !done) return fail(MI_E_INVALID, "null request");
+    *done = 1;
+    for (int i = 0; i < req->nev; i++) {
+        const hipError_t e = hipEventQuery(req->ev[i]);
+        if (e == hipErrorNotReady) {
+            (void)hipGetLastError();
+            *done = 0;
+        } else if (e != hipSuccess) {
+            return hip_fail(e, "hipEventQuery");
+        }
+    }
+    return 0;
+}
+
+int mi_wait(mi_request_t req) {
+    if (!req) return fail(MI_E_INVALID, "null request");
+    for (int i = 0; i < req->nev; i++) MI_HIP(hipEventSynchronize(req->ev[i]));
+    return 0;
+}
+
+int mi_request_free(mi_request_t req) {
+    if (!req) return 0;
+    for (int i = 0; i < req->nev; i++)
+        if (req->ev[i]) (void)hipEventDestroy(req->ev[i]);
+    delete req;
+    return 0;
+}
+
+// ---- in-process multi-GPU element-range shards -------------------------------
+int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs, int k, void* const* outs,
+                      const size_t* counts, int dtype, int op, unsigned flags) {
+    if (nshards < 1 || !devices || !inputs || !outs || !counts) return fail(MI_E_INVALID, "bad shard arguments");
+    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+    int prev = 0;
+    MI_HIP(hipGetDevice(&prev));
+    std::vector<DevCtx*> ctx((size_t)nshards, nullptr);
+    int rc = 0;
+    // launch every shard before waiting for any
+    for (int s = 0; s < nshards && rc == 0; s++) {
+        rc = get_ctx(devices[s], &ctx[s]);
+        if (rc) break;
+        hipError_t e = hipSetDevice(devices[s]);
+        if (e != hipSuccess) {
+            rc = hip_fail(e, "hipSetDevice");
+            break;
+        }
+        rc = launch_reduce(inputs + (size_t)s * k, k, outs[s], counts[s], dtype, op, flags, ctx[s]->stream[0]);
+    }
+    for (int s = 0; s < nshards; s++) {
+        if (!ctx[s]) continue;
+        (void)hipSetDevice(devices[s]);
+        const hipError_t e = hipStreamSynchronize(ctx[s]->stream[0]);
+        if (e != hipSuccess && rc == 0) rc = hip_fail(e, "hipStreamSynchronize");
+    }
+    (void)hipSetDevice(prev);
+    return rc;
 }
 
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {

@@ -1,0 +1,111 @@
+// dropin_caller.cpp — a C++ caller of the drop-in src/comp, written the way
+// oneCCL's schedule entries call it (src/sched/entry/recv_reduce_entry.hpp:
+// 113-132, reduce_local_entry.cpp:98-114): oneCCL types, the C++ entry
+// points resolved by their mangled names from libccl_comp_hip.so, buffers
+// from a host staging allocation (posix_memalign, like
+// sched->alloc_buffer -> src/common/utils/utils.hpp:109-117) and from
+// hipMalloc.  Checks results against closed forms.  Exit 0 = all pass.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../oneccl_amd/csrc/ccl_mirror.hpp"
+
+static int failures = 0;
+#define EXPECT(cond, ...)                         \
+    do {                                          \
+        if (!(cond)) {                            \
+            fprintf(stderr, "FAIL %s:%d ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);         \
+            fprintf(stderr, "\n");                \
+            failures++;                           \
+        }                                         \
+    } while (0)
+
+static void* staging_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, bytes)) return nullptr;
+    return p;
+}
+
+int main() {
+    const size_t n = 131072;  // C1: per-rank nreduce chunk of a 2-rank 1 MiB allreduce
+    const ccl_datatype f32(ccl::datatype::float32, sizeof(float));
+    const ccl::fn_context ctx = {"match", 0};
+
+    // host staging buffers (recv_reduce_entry's comm_buf and the accumulator)
+    float* comm_buf = static_cast<float*>(staging_alloc(n * sizeof(float)));
+    float* acc = static_cast<float*>(staging_alloc(n * sizeof(float)));
+    for (size_t i = 0; i < n; i++) {
+        comm_buf[i] = 1.0f;  // peer rank 1's chunk
+        acc[i] = 0.0f;       // own rank 0's chunk
+    }
+    ccl::status st = ccl_comp_reduce(nullptr, comm_buf, n, acc, nullptr, f32, ccl::reduction::sum, nullptr, &ctx);
+    EXPECT(st == ccl::status::success, "status %d", (int)st);
+    bool ok = true;
+    for (size_t i = 0; i < n; i++) ok = ok && acc[i] == 1.0f;  // (P-1)*P/2 with P = 2
+    EXPECT(ok, "host fp32 sum");
+
+    // device buffers: reduce_local_entry with device USM (reduce_local_entry.cpp:33-58)
+    float *din = nullptr, *dio = nullptr;
+    if (hipMalloc(&din, n * sizeof(float)) != hipSuccess || hipMalloc(&dio, n * sizeof(float)) != hipSuccess) {
+        fprintf(stderr, "hipMalloc failed\n");
+        return 2;
+    }
+    std::vector<float> h(n);
+    for (size_t i = 0; i < n; i++) h[i] = (float)(i % 1000);
+    (void)hipMemcpy(din, h.data(), n * sizeof(float), hipMemcpyHostToDevice);
+    for (size_t i = 0; i < n; i++) h[i] = (float)(i % 7);
+    (void)hipMemcpy(dio, h.data(), n * sizeof(float), hipMemcpyHostToDevice);
+    st = ccl_comp_reduce(nullptr, din, n, dio, nullptr, f32, ccl::reduction::max, nullptr, nullptr);
+    EXPECT(st == ccl::status::success, "status %d", (int)st);
+    (void)hipMemcpy(h.data(), dio, n * sizeof(float), hipMemcpyDeviceToHost);
+    ok = true;
+    for (size_t i = 0; i < n; i++) ok = ok && h[i] == std::fmax((float)(i % 1000), (float)(i % 7));
+    EXPECT(ok, "device fp32 max");
+
+    // bf16 with out_count (bf16.cpp:94-96) and in_count == 0 (comp.cpp:132-134)
+    std::vector<uint16_t> a(64, 0x3F80), b(64, 0x4000);  // 1.0 + 2.0
+    size_t out_count = 0;
+    ccl_comp_reduce(nullptr, a.data(), 64, b.data(), &out_count, ccl_datatype(ccl::datatype::bfloat16, 2),
+                    ccl::reduction::sum, nullptr, nullptr);
+    EXPECT(out_count == 64, "out_count %zu", out_count);
+    EXPECT(b[0] == 0x4040 && b[63] == 0x4040, "bf16 1+2 = %04x", b[0]);
+    EXPECT(ccl_comp_reduce(nullptr, a.data(), 0, b.data(), nullptr, f32, ccl::reduction::sum, nullptr, nullptr) ==
+               ccl::status::success,
+           "zero count");
+
+    // batch reduce: 4 int32 inputs, offsets in elements (comp.cpp:236-245)
+    std::vector<int32_t> packed(4 * 100);
+    for (int j = 0; j < 4; j++)
+        for (int i = 0; i < 100; i++) packed[j * 100 + i] = j + 1;
+    std::vector<int32_t> io(packed.begin(), packed.begin() + 100);
+    std::vector<size_t> offsets = {0, 100, 200, 300};
+    ccl_comp_batch_reduce(packed.data(), offsets, 100, io.data(), nullptr, ccl_datatype(ccl::datatype::int32, 4),
+                          ccl::reduction::prod, nullptr, nullptr, 0, nullptr, nullptr);
+    EXPECT(io[0] == 24 && io[99] == 24, "batch prod %d", io[0]);
+
+    // copy, to_str, custom op and its error
+    std::vector<char> src(1000, 'x'), dst(1000, 0);
+    ccl_comp_copy(src.data(), dst.data(), 1000, true);
+    EXPECT(memcmp(src.data(), dst.data(), 1000) == 0, "copy");
+    EXPECT(strcmp(ccl_reduction_to_str(ccl::reduction::prod), "prod") == 0, "to_str");
+    bool threw = false;
+    try {
+        ccl_comp_reduce(nullptr, a.data(), 64, b.data(), nullptr, f32, ccl::reduction::custom, nullptr, nullptr);
+    } catch (const ccl::exception&) {
+        threw = true;
+    }
+    EXPECT(threw, "custom without fn must throw (comp.cpp:85)");
+
+    free(comm_buf);
+    free(acc);
+    (void)hipFree(din);
+    (void)hipFree(dio);
+    printf("dropin_caller: %s (%d failures)\n", failures ? "FAIL" : "ok", failures);
+    return failures ? 1 : 0;
+}

@@ -1,0 +1,112 @@
+"""Asynchronous requests (mi_reduce_start / mi_test / mi_wait) and the
+in-process sharded multi-device call, against the oracle."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from oneccl_amd import _lib
+from tests.util import BF16, FP32, assert_same, from_dev, rand_array, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("where", ["device", "pageable", "pinned", "pinned_staged"])
+@pytest.mark.parametrize("n", [1000, (70 << 20) // 4 + 5])
+def test_start_test_wait(where, n):
+    import torch
+    m = _lib.mi()
+    a = rand_array(FP32, n, seed=1, specials=False)
+    b = rand_array(FP32, n, seed=2, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    keep = []
+    if where == "device":
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        keep += [ta, tb]
+    elif where.startswith("pinned"):
+        ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        pa, pb = ha.data_ptr(), hb.data_ptr()
+    else:
+        hb_np = b.copy()
+        pa, pb = a.ctypes.data, hb_np.ctypes.data
+    prev = m.mi_set_host_mode(1 if where == "pinned_staged" else 0)
+    try:
+        req = ctypes.c_void_p()
+        arr = _lib.void_ptr_array([pb, pa])
+        _lib.check(m.mi_reduce_start(arr, 2, pb, n, FP32, 0, 0, -1, ctypes.byref(req)))
+        done = ctypes.c_int(0)
+        polls = 0
+        while True:
+            _lib.check(m.mi_test(req, ctypes.byref(done)))
+            polls += 1
+            if done.value:
+                break
+            assert polls < 10_000_000
+        _lib.check(m.mi_wait(req))
+        _lib.check(m.mi_request_free(req))
+    finally:
+        m.mi_set_host_mode(prev)
+    if where == "device":
+        got = from_dev(tb, b)
+    elif where.startswith("pinned"):
+        got = hb.numpy().view(np.float32)
+    else:
+        got = hb_np
+    assert_same(got, exp, FP32, where)
+
+
+def test_many_outstanding_requests():
+    m = _lib.mi()
+    n = 1 << 20
+    reqs, outs, exps, keep = [], [], [], []
+    for j in range(8):
+        a = rand_array(BF16, n, seed=10 + j)
+        b = rand_array(BF16, n, seed=20 + j)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, BF16, 0, oracle.BF16_AVX512BF)
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        keep += [ta, tb]
+        r = ctypes.c_void_p()
+        _lib.check(m.mi_reduce_start(_lib.void_ptr_array([pb, pa]), 2, pb, n, BF16, 0, 0x3, -1, ctypes.byref(r)))
+        reqs.append(r)
+        outs.append((tb, b))
+        exps.append(exp)
+    for r in reqs:
+        _lib.check(m.mi_wait(r))
+        _lib.check(m.mi_request_free(r))
+    for (tb, b), exp in zip(outs, exps):
+        assert_same(from_dev(tb, b), exp, BF16)
+
+
+@pytest.mark.parametrize("nshards", [1, 2, 4, 8])
+def test_sharded_in_process(nshards):
+    """SURVEY §8e inside one process: every shard on its device (here all on
+    device 0 — the box has one GPU), launched together, no collective."""
+    import torch
+    m = _lib.mi()
+    n = 3_000_017
+    k = 3
+    ins = [rand_array(FP32, n, seed=40 + j) for j in range(k)]
+    exp = oracle.fanin(ins, FP32, 0)
+    dev_ins = [to_dev(x) for x in ins]
+    out_t, out_p = to_dev(np.zeros(n, np.float32))
+    ndev = torch.cuda.device_count()
+    devs, ptrs, outs, counts = [], [], [], []
+    for s in range(nshards):
+        lo = ctypes.c_size_t()
+        hi = ctypes.c_size_t()
+        _lib.check(m.mi_shard_range(n, s, nshards, 256, ctypes.byref(lo), ctypes.byref(hi)))
+        devs.append(s % ndev if ndev == 1 else 0)
+        ptrs += [p + 4 * lo.value for _, p in dev_ins]
+        outs.append(out_p + 4 * lo.value)
+        counts.append(hi.value - lo.value)
+    _lib.check(m.mi_reduce_sharded(nshards, (ctypes.c_int * nshards)(*devs), _lib.void_ptr_array(ptrs), k,
+                                   _lib.void_ptr_array(outs), (ctypes.c_size_t * nshards)(*counts), FP32, 0, 0))
+    assert_same(from_dev(out_t, ins[0]), exp, FP32)

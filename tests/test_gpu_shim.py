@@ -292,3 +292,17 @@ def test_reference_example_kats_through_dropin():
         elif c["suite"] == "examples/benchmark":
             assert kat.benchmark_case(
                 c, lambda a, b: comp.comp_reduce(ptr(a), a.size, ptr(b), comp.datatype.float32, comp.reduction.sum))
+
+
+def test_cpp_caller_links_dropin_by_mangled_names():
+    """A C++ program written like src/sched's call sites links
+    libccl_comp_hip.so and runs host and device reduces through it."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent / "cpp" / "dropin_caller"
+    if not exe.exists():
+        from oneccl_amd import build
+        build.build_dropin_caller()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "dropin_caller: ok" in r.stdout
