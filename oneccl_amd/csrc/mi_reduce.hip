@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <sched.h>
 #include <string>
 #include <vector>
 
@@ -48,6 +49,29 @@ constexpr int kMem = 3;     // non-temporal loads and stores (sweep: profiles/ro
 
 std::atomic<int> g_max_blocks{-1};  // -1 = not yet read from env; 0 = no cap
 std::atomic<int> g_host_mode{-1};   // -1 = not yet read from env
+
+std::atomic<int> g_sync_mode{-1};  // -1 = not yet read from env
+
+int sync_mode() {
+    int v = g_sync_mode.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* s = getenv("MI_REDUCE_SYNC");
+        v = (s && strcmp(s, "block") == 0) ? MI_SYNC_BLOCK : MI_SYNC_SPIN;
+        g_sync_mode.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
+// Wait for a stream: spin on hipStreamQuery (lowest latency for the
+// synchronous src/comp contract) or the runtime's blocking wait.
+hipError_t wait_stream(hipStream_t s) {
+    if (sync_mode() == MI_SYNC_BLOCK) return hipStreamSynchronize(s);
+    for (unsigned spins = 0;; spins++) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+        if (spins > 4096) sched_yield();
+    }
+}
 
 int host_mode() {
     int v = g_host_mode.load(std::memory_order_relaxed);
@@ -433,7 +457,7 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used);
     if (rc) return rc;
     for (int s = 0; s < 2; s++)
-        if (used & (1 << s)) MI_HIP(hipStreamSynchronize(d->stream[s]));
+        if (used & (1 << s)) MI_HIP(wait_stream(d->stream[s]));
     return 0;
 }
 
@@ -550,7 +574,7 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
     if (ks == PK_DEVICE && kd == PK_DEVICE) {
         rc = launch_convert(src, src_dtype, dst, dst_dtype, count, flags, d->stream[0], trunc_from);
         if (rc) return rc;
-        MI_HIP(hipStreamSynchronize(d->stream[0]));
+        MI_HIP(wait_stream(d->stream[0]));
         return 0;
     }
     const size_t ss = dtype_size(src_dtype), ds = dtype_size(dst_dtype);
@@ -577,8 +601,8 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
         if (rc) return rc;
         if (kd != PK_DEVICE) MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
     }
-    MI_HIP(hipStreamSynchronize(d->stream[0]));
-    MI_HIP(hipStreamSynchronize(d->stream[1]));
+    MI_HIP(wait_stream(d->stream[0]));
+    MI_HIP(wait_stream(d->stream[1]));
     return 0;
 }
 
@@ -673,7 +697,7 @@ int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs
     for (int s = 0; s < nshards; s++) {
         if (!ctx[s]) continue;
         (void)hipSetDevice(devices[s]);
-        const hipError_t e = hipStreamSynchronize(ctx[s]->stream[0]);
+        const hipError_t e = wait_stream(ctx[s]->stream[0]);
         if (e != hipSuccess && rc == 0) rc = hip_fail(e, "hipStreamSynchronize");
     }
     (void)hipSetDevice(prev);
@@ -720,14 +744,14 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
         if (prev != d->device) MI_HIP(hipSetDevice(d->device));
         rc = mi_copy(src, dst, bytes, nontemporal, d->stream[0]);
         if (!rc) {
-            hipError_t e = hipStreamSynchronize(d->stream[0]);
+            hipError_t e = wait_stream(d->stream[0]);
             if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
         }
         if (prev != d->device) (void)hipSetDevice(prev);
         return rc;
     }
     MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
-    MI_HIP(hipStreamSynchronize(d->stream[0]));
+    MI_HIP(wait_stream(d->stream[0]));
     return 0;
 }
 
@@ -780,6 +804,13 @@ int mi_set_host_mode(int mode) {
     if (mode < MI_HOST_AUTO || mode > MI_HOST_ZEROCOPY) return fail(MI_E_INVALID, "bad host mode");
     const int prev = host_mode();
     g_host_mode.store(mode == MI_HOST_ZEROCOPY ? MI_HOST_AUTO : mode, std::memory_order_relaxed);
+    return prev;
+}
+
+int mi_set_sync_mode(int mode) {
+    if (mode != MI_SYNC_SPIN && mode != MI_SYNC_BLOCK) return fail(MI_E_INVALID, "bad sync mode");
+    const int prev = sync_mode();
+    g_sync_mode.store(mode, std::memory_order_relaxed);
     return prev;
 }
 

@@ -312,7 +312,11 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
 // Grid-stride over tiles of kBlock*U vectors.  Block 0 also does the
 // scalar head/tail (< 16 elements each).  `scalar_only` = operands with
 // different misalignments: plain element loop.
-template <typename Tag, int OP, unsigned V, int KT, int U, int MEM>
+// MAP 1: blocks b, b+8, b+16, ... (one XCD under the observed round-robin
+// dispatch, MI355X_MICROARCH.md §Workgroup dispatch) take one contiguous
+// 1/8 of the tiles (grid must be a multiple of 8; speed only, never
+// correctness: every tile is still covered exactly once).
+template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(KArgs a) {
     const int k = (KT > 0) ? KT : a.k;
     if (a.scalar_only) {
@@ -329,7 +333,9 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(KArgs a) {
     }
     const uint64_t tile = (uint64_t)kBlock * U;
     const uint64_t stride = (uint64_t)gridDim.x * tile;
-    for (uint64_t base = (uint64_t)blockIdx.x * tile; base < a.nvec; base += stride) {
+    uint64_t b = blockIdx.x;
+    if constexpr (MAP == 1) b = (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+    for (uint64_t base = b * tile; base < a.nvec; base += stride) {
         if (base + tile <= a.nvec)
             reduce_tile<Tag, OP, V, KT, U, MEM, false>(a, k, base + threadIdx.x);
         else

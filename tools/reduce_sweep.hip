@@ -28,6 +28,33 @@ using namespace mi;
         }                                                                                \
     } while (0)
 
+// Streaming ceilings on this device: read-only (2 streams, nt loads, one
+// float per block written so nothing is dead) and write-only (nt stores).
+__global__ __launch_bounds__(kBlock) void read2_kernel(const u32x4* a, const u32x4* b, uint64_t nvec, float* sink) {
+    constexpr int U = 4;
+    const uint64_t base = (uint64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = base + (uint64_t)j * kBlock;
+        if (v < nvec) {
+            u32x4 x = __builtin_nontemporal_load(a + v), y = __builtin_nontemporal_load(b + v);
+            acc += __uint_as_float(x[0] ^ y[1]) + __uint_as_float(x[2] ^ y[3]);
+        }
+    }
+    if (acc == 1.2345f) sink[blockIdx.x] = acc;  // practically never taken; keeps the loads live
+}
+
+__global__ __launch_bounds__(kBlock) void write_kernel(u32x4* o, uint64_t nvec) {
+    constexpr int U = 4;
+    const uint64_t base = (uint64_t)blockIdx.x * kBlock * U + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = base + (uint64_t)j * kBlock;
+        if (v < nvec) __builtin_nontemporal_store(u32x4{(uint32_t)v, 1u, 2u, 3u}, o + v);
+    }
+}
+
 struct Variant {
     std::string name;
     double traffic;  // bytes per launch
@@ -48,14 +75,15 @@ void add_reduce(std::vector<Variant>& vs, KArgs a, int cap, double traffic) {
                   }, {}});
 }
 
-template <int KT, int U>
+template <int KT, int U, int MAP = 0>
 void add_fanin(std::vector<Variant>& vs, KArgs a, double traffic) {
     const uint64_t tile = (uint64_t)kBlock * U;
-    const uint64_t blocks = (a.nvec + tile - 1) / tile;
+    uint64_t blocks = (a.nvec + tile - 1) / tile;
+    if (MAP) blocks = (blocks + 7) / 8 * 8;
     char name[128];
-    snprintf(name, sizeof name, "fanin8 KT=%d U=%d mem=3 grid=%llu", KT, U, (unsigned long long)blocks);
+    snprintf(name, sizeof name, "fanin KT=%d U=%d mem=3 map=%d grid=%llu", KT, U, MAP, (unsigned long long)blocks);
     vs.push_back({name, traffic, [a, blocks](hipStream_t s) {
-                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, KT, U, 3>), dim3((unsigned)blocks),
+                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, KT, U, 3, MAP>), dim3((unsigned)blocks),
                                          dim3(kBlock), 0, s, a);
                   }, {}});
 }
@@ -86,14 +114,10 @@ int main(int argc, char** argv) {
     const double t3 = 3.0 * bytes;
 
     std::vector<Variant> vs;
-    const int caps[] = {0, 512, 2048};
-    for (int cap : caps) {
-        add_reduce<1, 3>(vs, a, cap, t3);
-        add_reduce<2, 3>(vs, a, cap, t3);
-        add_reduce<4, 2>(vs, a, cap, t3);
-        add_reduce<4, 3>(vs, a, cap, t3);
-        add_reduce<8, 3>(vs, a, cap, t3);
-    }
+    add_reduce<4, 3>(vs, a, 0, t3);  // the library's configuration
+    add_reduce<2, 3>(vs, a, 0, t3);
+    add_reduce<4, 2>(vs, a, 0, t3);
+    add_reduce<4, 3>(vs, a, 512, t3);
     // 8-input fan-in (C4): 7 more input buffers, one output
     std::vector<float*> fan(8, nullptr);
     fan[0] = io;
@@ -111,11 +135,35 @@ int main(int argc, char** argv) {
     f8.trunc_from = n;
     const double t9 = 9.0 * bytes;
     add_fanin<0, 4>(vs, f8, t9);
-    add_fanin<8, 1>(vs, f8, t9);
-    add_fanin<8, 2>(vs, f8, t9);
-    add_fanin<8, 4>(vs, f8, t9);
-    add_fanin<0, 2>(vs, f8, t9);
-    add_fanin<0, 1>(vs, f8, t9);
+    add_fanin<0, 4, 1>(vs, f8, t9);
+    // rate vs number of input streams (runtime K, same kernel)
+    for (int kk : {3, 4, 6}) {
+        KArgs fk = f8;
+        fk.k = kk;
+        add_fanin<0, 4>(vs, fk, (kk + 1.0) * bytes);
+        vs.back().name += " k=" + std::to_string(kk);
+    }
+    // rate vs bucket size at K = 8 (footprint / TLB reach)
+    for (size_t div : {4, 16}) {
+        KArgs fs = f8;
+        fs.count = n / div;
+        fs.nvec = fs.count / 4;
+        add_fanin<0, 4>(vs, fs, 9.0 * bytes / div);
+        vs.back().name += " bucket/" + std::to_string(div);
+    }
+    {
+        const uint64_t nvec = bytes / 16;
+        const uint64_t blocks = (nvec + kBlock * 4 - 1) / (kBlock * 4);
+        float* sink = cp;
+        vs.push_back({"read-only 2 streams (nt)", 2.0 * bytes, [=](hipStream_t st) {
+                          hipLaunchKernelGGL(read2_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                                             (const u32x4*)in, (const u32x4*)io, nvec, sink);
+                      }, {}});
+        vs.push_back({"write-only 1 stream (nt)", 1.0 * bytes, [=](hipStream_t st) {
+                          hipLaunchKernelGGL(write_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                                             (u32x4*)cp, nvec);
+                      }, {}});
+    }
     vs.push_back({"hipMemcpyAsync D2D", 2.0 * bytes,
                   [=](hipStream_t st) { (void)hipMemcpyAsync(cp, in, bytes, hipMemcpyDeviceToDevice, st); }, {}});
     for (int mem : {0, 2}) {

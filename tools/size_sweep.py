@@ -61,16 +61,17 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             kern_us = e0.elapsed_time(e1) * 1e3 / reps
-            # synchronous drop-in path on device buffers
-            t = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                m.mi_reduce_sync(a.data_ptr(), b.data_ptr(), n, dt, op, 0, -1)
-                t.append(time.perf_counter() - t0)
-            sync_us = min(t) * 1e6
+            # synchronous drop-in path on device buffers, spin and blocking waits
             row = {"config": name, "bytes": nbytes, "elems": n, "kernel_us": round(kern_us, 2),
-                   "kernel_GBps_3x": round(3 * nbytes / (kern_us * 1e-6) / 1e9, 1),
-                   "sync_device_us": round(sync_us, 2)}
+                   "kernel_GBps_3x": round(3 * nbytes / (kern_us * 1e-6) / 1e9, 1)}
+            for mode, key in ((1, "sync_device_block_us"), (0, "sync_device_us")):
+                m.mi_set_sync_mode(mode)
+                t = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    m.mi_reduce_sync(a.data_ptr(), b.data_ptr(), n, dt, op, 0, -1)
+                    t.append(time.perf_counter() - t0)
+                row[key] = round(min(t) * 1e6, 2)
             if nbytes <= (256 << 20):
                 ha = torch.ones(n, dtype=tdt).pin_memory()
                 hb = torch.ones(n, dtype=tdt).pin_memory()
