@@ -207,11 +207,10 @@ int mi_pointer_kind(const void* ptr, int* device);
 #define MI_HOST_ZEROCOPY 2
 int mi_set_host_mode(int mode);
 
-/* How the synchronous entry points wait for the GPU: MI_SYNC_SPIN (default)
- * polls the stream (lowest latency; the caller's worker thread is busy-
- * waiting anyway in oneCCL, src/exec/thread/worker.cpp:341-374),
- * MI_SYNC_BLOCK uses the runtime's blocking wait.  Env MI_REDUCE_SYNC=
- * spin|block.  Returns the previous mode.                                  */
+/* How the synchronous entry points wait for the GPU: MI_SYNC_BLOCK (default)
+ * uses the runtime's stream wait; MI_SYNC_SPIN polls hipStreamQuery (was
+ * 1-2 us slower per call on MI355X / ROCm 7.2, profiles/round1_size_sweep2
+ * .jsonl).  Env MI_REDUCE_SYNC=spin|block.  Returns the previous mode.     */
 #define MI_SYNC_SPIN 0
 #define MI_SYNC_BLOCK 1
 int mi_set_sync_mode(int mode);

@@ -56,7 +56,7 @@ int sync_mode() {
     int v = g_sync_mode.load(std::memory_order_relaxed);
     if (v < 0) {
         const char* s = getenv("MI_REDUCE_SYNC");
-        v = (s && strcmp(s, "block") == 0) ? MI_SYNC_BLOCK : MI_SYNC_SPIN;
+        v = (s && strcmp(s, "spin") == 0) ? MI_SYNC_SPIN : MI_SYNC_BLOCK;
         g_sync_mode.store(v, std::memory_order_relaxed);
     }
     return v;

@@ -280,7 +280,7 @@ int orc_comp_reduce_mt(const void* in_buf, size_t n, void* inout_buf, int dtype,
         return orc_comp_reduce(in_buf, n, inout_buf, NULL, dtype, op, bf16_impl, fp16_impl);
     orc_part_t* parts = (orc_part_t*)calloc((size_t)nthreads, sizeof(orc_part_t));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
-    size_t per = (n / (size_t)nthreads + 63) / 64 * 64;
+    size_t per = ((n + (size_t)nthreads - 1) / (size_t)nthreads + 63) / 64 * 64;
     int rc = 0;
     for (int t = 0; t < nthreads; t++) {
         size_t b = (size_t)t * per, e = b + per;

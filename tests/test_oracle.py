@@ -164,8 +164,8 @@ def test_batch_storage_equals_chain():
         assert (oc == n) == (dt in (BF16, FP16))  # out_count written only by bf16/fp16 (bf16.cpp:94-96)
 
 
-def test_mt_equals_single_thread():
-    n = 1 << 20
+@pytest.mark.parametrize("n", [1 << 20, (70 << 20) // 4 + 5, 64 * 8 + 1, 777])
+def test_mt_equals_single_thread(n):
     a = rand_array(FP32, n, seed=1)
     b = rand_array(FP32, n, seed=2)
     e1 = b.copy()
