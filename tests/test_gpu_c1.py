@@ -7,8 +7,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["chained", "fused_batch"])
 @pytest.mark.parametrize("ranks,count", [(2, 262144), (4, 262144), (2, 17 * 2)])
-def test_c1_allreduce_through_dropin(ranks, count):
+def test_c1_allreduce_through_dropin(ranks, count, fused):
     from tools.c1_allreduce import run
-    r = run(ranks, count, 3, "dropin")
+    r = run(ranks, count, 3, "dropin", fused)
     assert r["correct"], r

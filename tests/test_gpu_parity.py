@@ -226,3 +226,31 @@ def test_full_c4_fanin8_fp32_1gib():
     _sync()
     got = to.cpu().numpy().view(np.float32)
     assert_same(got, exp, FP32, "C4")
+
+
+@pytest.mark.parametrize("dt,n", [(0, (1 << 32) + 4099), (BF16, (1 << 31) + 77)],
+                         ids=["int8-2^32+", "bf16-2^31+"])
+def test_counts_beyond_32_bit_indices(dt, n):
+    """Element counts past 2^31 / 2^32 (288 GB HBM makes them practical).  The
+    reference's bf16/fp16 loops index with `int` and break above 2^31
+    (bf16_intrisics.hpp:108); the kernels index with 64 bits."""
+    import torch
+    rng = np.random.default_rng(9)
+    st = oracle.NP_DTYPE[dt]
+    if dt == BF16:
+        a = oracle.f32_to_bf16(rng.standard_normal(n, dtype=np.float32), True)
+        b = oracle.f32_to_bf16(rng.standard_normal(n, dtype=np.float32), True)
+    else:
+        a = rng.integers(-128, 128, n, dtype=st)
+        b = rng.integers(-128, 128, n, dtype=st)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 16, oracle.BF16_AVX512BF)
+    flags = bf16_flags(2) if dt == BF16 else 0
+    ta = torch.from_numpy(a.view(np.int8 if dt == 0 else np.int16)).cuda()
+    del a
+    tb = torch.from_numpy(b.view(np.int8 if dt == 0 else np.int16)).cuda()
+    del b
+    _lib.check(_lib.mi().mi_reduce(ta.data_ptr(), tb.data_ptr(), n, dt, 0, flags, _stream()))
+    _sync()
+    got = tb.cpu().numpy().view(st)
+    assert_same(got, exp, dt, f"n={n}")

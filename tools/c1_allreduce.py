@@ -29,9 +29,11 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
-def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs):
+def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs, fused=None):
     """In-place allreduce of a float32 host tensor (nreduce schedule); the
-    element count must be a multiple of the rank count."""
+    element count must be a multiple of the rank count.  `fused(recv_all,
+    own)`, if given, folds all arrived chunks with one ccl_comp_batch_reduce
+    call instead of world-1 chained ccl_comp_reduce calls."""
     import torch
     import torch.distributed as dist
     n = buf.numel()
@@ -46,9 +48,12 @@ def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs):
             reqs.append(dist.irecv(recv_bufs[peer], peer))
     for r in reqs:
         r.wait()
-    for peer in range(world):  # fold each peer's chunk into the owned chunk
-        if peer != rank:
-            reduce2(recv_bufs[peer], own)
+    if fused is not None:
+        fused(rank, own)
+    else:
+        for peer in range(world):  # fold each peer's chunk into the owned chunk
+            if peer != rank:
+                reduce2(recv_bufs[peer], own)
     gathered = [torch.empty_like(own) for _ in range(world)]
     dist.all_gather(gathered, own)
     for i, g in enumerate(gathered):
@@ -56,7 +61,7 @@ def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs):
             chunks[i].copy_(g)
 
 
-def worker(rank, world, port, count, iters, mode, q):
+def worker(rank, world, port, count, iters, mode, q, fused_call=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import numpy as np
     import torch
@@ -76,7 +81,23 @@ def worker(rank, world, port, count, iters, mode, q):
                 oracle.comp_reduce(inp.numpy(), inout.numpy(), 9, 0)
 
         per = count // world
-        recv = {p: torch.empty(per, dtype=torch.float32) for p in range(world)}
+        recv_all = torch.empty(world * per, dtype=torch.float32)  # one staging area, chunk p at p*per
+        recv = {p: recv_all[p * per:(p + 1) * per] for p in range(world)}
+        fused = None
+        if fused_call:
+            if mode == "dropin":
+                from oneccl_amd import comp
+
+                def fused(r, own):
+                    offs = [0] + [p * per for p in range(world) if p != r]  # offsets[0] unused
+                    comp.comp_batch_reduce(recv_all.data_ptr(), offs, per, own.data_ptr(), comp.datatype.float32,
+                                           comp.reduction.sum)
+            else:
+                import oracle
+
+                def fused(r, own):
+                    offs = [0] + [p * per for p in range(world) if p != r]
+                    oracle.batch_reduce(recv_all.numpy(), offs, per, own.numpy(), 9, 0, 0)
         buf = torch.empty(count, dtype=torch.float32)
         ok = True
         times = []
@@ -84,7 +105,7 @@ def worker(rank, world, port, count, iters, mode, q):
             buf.fill_(float(rank))
             dist.barrier()
             t0 = time.perf_counter()
-            nreduce_allreduce(buf, rank, world, reduce2, recv)
+            nreduce_allreduce(buf, rank, world, reduce2, recv, fused)
             dist.barrier()
             if it >= 3:
                 times.append(time.perf_counter() - t0)
@@ -96,7 +117,7 @@ def worker(rank, world, port, count, iters, mode, q):
         dist.destroy_process_group()
 
 
-def run(world=2, count=262144, iters=50, mode="dropin"):
+def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -104,17 +125,19 @@ def run(world=2, count=262144, iters=50, mode="dropin"):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, world, port, count, iters, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, count, iters, mode, q, fused_call))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=600) for _ in range(world)])
     for p in procs:
         p.join(timeout=60)
     return {"config": "examples/benchmark allreduce fp32 sum, loopback (BASELINE configs[0])", "ranks": world,
-            "count": count, "bytes": count * 4, "local_reduce": mode, "iters": iters,
+            "count": count, "bytes": count * 4, "local_reduce": mode, "fused_batch_reduce": fused_call,
+            "iters": iters,
             "correct": all(r[1] for r in res) and all(p.exitcode == 0 for p in procs),
             "best_us": round(res[0][2][0] * 1e6, 1), "median_us": round(res[0][2][1] * 1e6, 1),
-            "reduce_calls_per_rank": world - 1, "reduce_elems_per_call": (count + world - 1) // world}
+            "reduce_calls_per_rank": 1 if fused_call else world - 1, "reduce_elems_per_call": count // world}
 
 
 if __name__ == "__main__":
@@ -123,5 +146,6 @@ if __name__ == "__main__":
     ap.add_argument("--count", type=int, default=262144)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--reduce", default="dropin", choices=["dropin", "oracle"])
+    ap.add_argument("--fused", action="store_true", help="one ccl_comp_batch_reduce per rank")
     a = ap.parse_args()
-    print(json.dumps(run(a.ranks, a.count, a.iters, a.reduce)), flush=True)
+    print(json.dumps(run(a.ranks, a.count, a.iters, a.reduce, a.fused)), flush=True)

@@ -39,7 +39,10 @@ for step in "$@"; do
             run bench 600 python bench.py ;;
         c1)
             run c1_dropin 300 python tools/c1_allreduce.py --reduce dropin &&
-            run c1_oracle 300 python tools/c1_allreduce.py --reduce oracle ;;
+            run c1_oracle 300 python tools/c1_allreduce.py --reduce oracle &&
+            run c1_dropin_p4 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 &&
+            run c1_dropin_p4_fused 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 --fused &&
+            run c1_oracle_p4 300 python tools/c1_allreduce.py --reduce oracle --ranks 4 ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
         benchall)
