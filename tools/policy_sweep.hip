@@ -72,6 +72,28 @@ __global__ __launch_bounds__(B) void k_global(const u32x4* in, u32x4* io, uint32
     }
 }
 
+// write-only streams: store form / cache bits / tile size
+template <int B, int U, int SP>
+__global__ __launch_bounds__(B) void w_buffer(float* o, uint32_t tiles) {
+    const uint32_t t = blockIdx.x;
+    if (t >= tiles) return;
+    const size_t tb = (size_t)B * U * 16;
+    char* po = reinterpret_cast<char*>(o) + t * tb;
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)po, (short)0, (int)tb, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{t, (uint32_t)j, threadIdx.x, 7u}, ro, (threadIdx.x + j * B) * 16, 0, SP);
+}
+
+template <int B, int U>
+__global__ __launch_bounds__(B) void w_b64(uint64_t* o, uint32_t tiles) {  // 8-byte stores, nt
+    const uint32_t t = blockIdx.x;
+    if (t >= tiles) return;
+    const size_t base = (size_t)t * B * U * 2 + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 2 * U; j++) __builtin_nontemporal_store((uint64_t)(base + j), o + base + (size_t)j * B);
+}
+
 struct Variant {
     std::string name;
     std::function<void(hipStream_t)> run;
@@ -127,35 +149,27 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
 
     std::vector<Variant> vs;
-    addg<256, 4, 1, 0>(vs);  // == the library's current best
-    addg<256, 4, 1, 1>(vs);
-    addg<512, 4, 1, 0>(vs);
-    addg<1024, 4, 1, 0>(vs);
-    addg<256, 2, 1, 0>(vs);
-    addg<256, 8, 1, 0>(vs);
-    addg<512, 2, 1, 0>(vs);
-    addg<1024, 2, 1, 0>(vs);
+    addg<256, 4, 1, 0>(vs);  // == the library's configuration
     addg<1024, 1, 1, 0>(vs);
-    addg<512, 8, 1, 0>(vs);
-    addg<256, 16, 1, 0>(vs);
     addb<256, 4, 2, 2, 0>(vs);
-    addb<256, 4, 3, 2, 0>(vs);
-    addb<256, 4, 18, 2, 0>(vs);
-    addb<256, 4, 19, 2, 0>(vs);
-    addb<256, 4, 16, 2, 0>(vs);
     addb<256, 4, 2, 18, 0>(vs);
-    addb<256, 4, 2, 3, 0>(vs);
-    addb<256, 4, 2, 19, 0>(vs);
-    addb<256, 4, 2, 16, 0>(vs);
-    addb<256, 4, 2, 0, 0>(vs);
-    addb<256, 4, 0, 2, 0>(vs);
-    addb<256, 4, 2, 2, 1>(vs);
-    addb<512, 4, 2, 2, 0>(vs);
-    addb<1024, 4, 2, 2, 0>(vs);
-    addb<256, 8, 2, 2, 0>(vs);
-    addb<512, 8, 2, 2, 0>(vs);
-    addb<1024, 2, 2, 2, 0>(vs);
 
+    {
+        float* wo = io;
+        auto addw = [&](const char* name, std::function<void(hipStream_t)> f) {
+            vs.push_back({name, f, {}});
+            vs.back().name = std::string("WRITE-ONLY ") + name;
+        };
+        const uint32_t t4 = (uint32_t)(g_nvec / (256 * 4)), t16 = (uint32_t)(g_nvec / (256 * 16));
+        addw("buffer B=256 U=4 st=nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 2>), dim3(t4), dim3(256), 0, st, wo, t4); });
+        addw("buffer B=256 U=4 st=plain", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 0>), dim3(t4), dim3(256), 0, st, wo, t4); });
+        addw("buffer B=256 U=4 st=sc1", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 16>), dim3(t4), dim3(256), 0, st, wo, t4); });
+        addw("buffer B=256 U=4 st=sc0sc1", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 17>), dim3(t4), dim3(256), 0, st, wo, t4); });
+        addw("buffer B=256 U=4 st=sc1nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 18>), dim3(t4), dim3(256), 0, st, wo, t4); });
+        addw("buffer B=256 U=16 st=nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 16, 2>), dim3(t16), dim3(256), 0, st, wo, t16); });
+        addw("b64 B=256 U=4 nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_b64<256, 4>), dim3(t4), dim3(256), 0, st, (uint64_t*)wo, t4); });
+        addw("hipMemsetAsync", [=](hipStream_t st) { (void)hipMemsetAsync(wo, 0, g_nvec * 16, st); });
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -176,8 +190,8 @@ int main(int argc, char** argv) {
         }
         fprintf(stderr, "round %d/%d\n", r + 1, rounds);
     }
-    const double traffic = 3.0 * bytes;
     for (auto& v : vs) {
+        const double traffic = (v.name.rfind("WRITE-ONLY", 0) == 0 ? 1.0 : 3.0) * bytes;
         std::sort(v.ms.begin(), v.ms.end());
         const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
         printf("{\"variant\": \"%s\", \"median_ms\": %.5f, \"best_ms\": %.5f, \"median_GBps\": %.1f, "
