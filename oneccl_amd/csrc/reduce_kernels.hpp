@@ -227,8 +227,8 @@ __device__ __forceinline__ void reduce_elem(const KArgs& a, int k, uint64_t idx)
     static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
 }
 
-// One tile row: U vectors per lane at v0, v0+kBlock, ...  GUARD = last tile.
-template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, bool GUARD>
+// One tile row: U vectors per lane at v0, v0+B, ...  GUARD = last tile.
+template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, bool GUARD, int B>
 __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
@@ -244,7 +244,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
     // issue input 0 and input 1 loads back to back (2*U*16 B in flight per lane)
 #pragma unroll
     for (int j = 0; j < U; j++) {
-        const uint64_t v = v0 + (uint64_t)j * kBlock;
+        const uint64_t v = v0 + (uint64_t)j * B;
         if (!GUARD || v < a.nvec) {
             u32x4 r = vload<MEM>(p0 + v);
             Pack<S> p = __builtin_bit_cast(Pack<S>, r);
@@ -255,7 +255,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
     if (KT == 2 || k >= 2) {
 #pragma unroll
         for (int j = 0; j < U; j++) {
-            const uint64_t v = v0 + (uint64_t)j * kBlock;
+            const uint64_t v = v0 + (uint64_t)j * B;
             cur[j] = u32x4{0u, 0u, 0u, 0u};
             if (!GUARD || v < a.nvec) cur[j] = vload<MEM>(p1 + v);
         }
@@ -277,7 +277,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
                     reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[i + 1]) + hb);
 #pragma unroll
                 for (int j = 0; j < U; j++) {
-                    const uint64_t v = v0 + (uint64_t)j * kBlock;
+                    const uint64_t v = v0 + (uint64_t)j * B;
                     nxt[j] = u32x4{0u, 0u, 0u, 0u};
                     if (!GUARD || v < a.nvec) nxt[j] = vload<MEM>(pn + v);
                 }
@@ -298,7 +298,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
     u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
 #pragma unroll
     for (int j = 0; j < U; j++) {
-        const uint64_t v = v0 + (uint64_t)j * kBlock;
+        const uint64_t v = v0 + (uint64_t)j * B;
         if (!GUARD || v < a.nvec) {
             Pack<S> p;
 #pragma unroll
@@ -309,19 +309,19 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
     }
 }
 
-// Grid-stride over tiles of kBlock*U vectors.  Block 0 also does the
+// Grid-stride over tiles of B*U vectors (B threads per block).  Block 0 also does the
 // scalar head/tail (< 16 elements each).  `scalar_only` = operands with
 // different misalignments: plain element loop.
 // MAP 1: blocks b, b+8, b+16, ... (one XCD under the observed round-robin
 // dispatch, MI355X_MICROARCH.md §Workgroup dispatch) take one contiguous
 // 1/8 of the tiles (grid must be a multiple of 8; speed only, never
 // correctness: every tile is still covered exactly once).
-template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, int MAP = 0>
-__global__ __launch_bounds__(kBlock) void reduce_kernel(KArgs a) {
+template <typename Tag, int OP, unsigned V, int KT, int U, int MEM, int MAP = 0, int B = kBlock>
+__global__ __launch_bounds__(B) void reduce_kernel(KArgs a) {
     const int k = (KT > 0) ? KT : a.k;
     if (a.scalar_only) {
-        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.count;
-             i += (uint64_t)gridDim.x * kBlock)
+        for (uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x; i < a.count;
+             i += (uint64_t)gridDim.x * B)
             reduce_elem<Tag, OP, V>(a, k, i);
         return;
     }
@@ -331,15 +331,15 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(KArgs a) {
         if (threadIdx.x < a.head) reduce_elem<Tag, OP, V>(a, k, threadIdx.x);
         if (threadIdx.x < a.tail) reduce_elem<Tag, OP, V>(a, k, a.head + a.nvec * N + threadIdx.x);
     }
-    const uint64_t tile = (uint64_t)kBlock * U;
+    const uint64_t tile = (uint64_t)B * U;
     const uint64_t stride = (uint64_t)gridDim.x * tile;
     uint64_t b = blockIdx.x;
     if constexpr (MAP == 1) b = (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
     for (uint64_t base = b * tile; base < a.nvec; base += stride) {
         if (base + tile <= a.nvec)
-            reduce_tile<Tag, OP, V, KT, U, MEM, false>(a, k, base + threadIdx.x);
+            reduce_tile<Tag, OP, V, KT, U, MEM, false, B>(a, k, base + threadIdx.x);
         else
-            reduce_tile<Tag, OP, V, KT, U, MEM, true>(a, k, base + threadIdx.x);
+            reduce_tile<Tag, OP, V, KT, U, MEM, true, B>(a, k, base + threadIdx.x);
     }
 }
 

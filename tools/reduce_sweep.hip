@@ -62,29 +62,31 @@ struct Variant {
     std::vector<float> ms;
 };
 
-template <int U, int MEM>
+template <int U, int MEM, int B = kBlock>
 void add_reduce(std::vector<Variant>& vs, KArgs a, int cap, double traffic) {
-    const uint64_t tile = (uint64_t)kBlock * U;
+    const uint64_t tile = (uint64_t)B * U;
     uint64_t blocks = (a.nvec + tile - 1) / tile;
     if (cap > 0) blocks = std::min<uint64_t>(blocks, cap);
     char name[128];
-    snprintf(name, sizeof name, "reduce U=%d mem=%d grid=%s%llu", U, MEM, cap ? "cap" : "", (unsigned long long)blocks);
+    snprintf(name, sizeof name, "reduce B=%d U=%d mem=%d grid=%s%llu", B, U, MEM, cap ? "cap" : "",
+             (unsigned long long)blocks);
     vs.push_back({name, traffic, [a, blocks](hipStream_t s) {
-                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, 2, U, MEM>), dim3((unsigned)blocks),
-                                         dim3(kBlock), 0, s, a);
+                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, 2, U, MEM, 0, B>), dim3((unsigned)blocks),
+                                         dim3(B), 0, s, a);
                   }, {}});
 }
 
-template <int KT, int U, int MAP = 0>
+template <int KT, int U, int MAP = 0, int B = kBlock>
 void add_fanin(std::vector<Variant>& vs, KArgs a, double traffic) {
-    const uint64_t tile = (uint64_t)kBlock * U;
+    const uint64_t tile = (uint64_t)B * U;
     uint64_t blocks = (a.nvec + tile - 1) / tile;
     if (MAP) blocks = (blocks + 7) / 8 * 8;
     char name[128];
-    snprintf(name, sizeof name, "fanin KT=%d U=%d mem=3 map=%d grid=%llu", KT, U, MAP, (unsigned long long)blocks);
+    snprintf(name, sizeof name, "fanin B=%d KT=%d U=%d mem=3 map=%d grid=%llu", B, KT, U, MAP,
+             (unsigned long long)blocks);
     vs.push_back({name, traffic, [a, blocks](hipStream_t s) {
-                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, KT, U, 3, MAP>), dim3((unsigned)blocks),
-                                         dim3(kBlock), 0, s, a);
+                      hipLaunchKernelGGL((reduce_kernel<float, OP_SUM, 0u, KT, U, 3, MAP, B>), dim3((unsigned)blocks),
+                                         dim3(B), 0, s, a);
                   }, {}});
 }
 
@@ -114,10 +116,15 @@ int main(int argc, char** argv) {
     const double t3 = 3.0 * bytes;
 
     std::vector<Variant> vs;
-    add_reduce<4, 3>(vs, a, 0, t3);  // the library's configuration
-    add_reduce<2, 3>(vs, a, 0, t3);
-    add_reduce<4, 2>(vs, a, 0, t3);
-    add_reduce<4, 3>(vs, a, 512, t3);
+    add_reduce<4, 3, 256>(vs, a, 0, t3);  // the library's configuration
+    add_reduce<1, 3, 256>(vs, a, 0, t3);
+    add_reduce<2, 3, 256>(vs, a, 0, t3);
+    add_reduce<1, 3, 512>(vs, a, 0, t3);
+    add_reduce<2, 3, 512>(vs, a, 0, t3);
+    add_reduce<4, 3, 512>(vs, a, 0, t3);
+    add_reduce<1, 3, 1024>(vs, a, 0, t3);
+    add_reduce<2, 3, 1024>(vs, a, 0, t3);
+    add_reduce<4, 3, 1024>(vs, a, 0, t3);
     // 8-input fan-in (C4): 7 more input buffers, one output
     std::vector<float*> fan(8, nullptr);
     fan[0] = io;
@@ -135,22 +142,10 @@ int main(int argc, char** argv) {
     f8.trunc_from = n;
     const double t9 = 9.0 * bytes;
     add_fanin<0, 4>(vs, f8, t9);
-    add_fanin<0, 4, 1>(vs, f8, t9);
-    // rate vs number of input streams (runtime K, same kernel)
-    for (int kk : {3, 4, 6}) {
-        KArgs fk = f8;
-        fk.k = kk;
-        add_fanin<0, 4>(vs, fk, (kk + 1.0) * bytes);
-        vs.back().name += " k=" + std::to_string(kk);
-    }
-    // rate vs bucket size at K = 8 (footprint / TLB reach)
-    for (size_t div : {4, 16}) {
-        KArgs fs = f8;
-        fs.count = n / div;
-        fs.nvec = fs.count / 4;
-        add_fanin<0, 4>(vs, fs, 9.0 * bytes / div);
-        vs.back().name += " bucket/" + std::to_string(div);
-    }
+    add_fanin<0, 1, 0, 1024>(vs, f8, t9);
+    add_fanin<0, 2, 0, 1024>(vs, f8, t9);
+    add_fanin<0, 2, 0, 512>(vs, f8, t9);
+    add_fanin<8, 1, 0, 1024>(vs, f8, t9);
     {
         const uint64_t nvec = bytes / 16;
         const uint64_t blocks = (nvec + kBlock * 4 - 1) / (kBlock * 4);
@@ -163,6 +158,8 @@ int main(int argc, char** argv) {
                           hipLaunchKernelGGL(write_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st,
                                              (u32x4*)cp, nvec);
                       }, {}});
+        vs.push_back({"hipMemsetAsync (write-only)", 1.0 * bytes,
+                      [=](hipStream_t st) { (void)hipMemsetAsync(cp, 0, bytes, st); }, {}});
     }
     vs.push_back({"hipMemcpyAsync D2D", 2.0 * bytes,
                   [=](hipStream_t st) { (void)hipMemcpyAsync(cp, in, bytes, hipMemcpyDeviceToDevice, st); }, {}});
