@@ -344,6 +344,69 @@ __global__ __launch_bounds__(B) void reduce_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Lean 2-input kernel (the ccl_comp_reduce case): one tile of B*U vectors per
+// block, three pointers, no grid-stride loop.  Per-thread work is a handful
+// of address ops around the loads — with 1-vector-per-lane tiles the general
+// kernel's argument block and loop structure cost 10-15 % of HBM rate
+// (profiles/round1_sweep5_block.jsonl).  Block 0 also does the scalar head
+// and tail.  Same element semantics as reduce_kernel (step / finish).
+// ---------------------------------------------------------------------------
+struct R2Args {
+    const void* acc;  // the `inout` role (accumulator start)
+    const void* in;   // the `in` role
+    void* out;
+    uint64_t nvec;        // 16-byte vectors in the aligned body
+    uint32_t head, tail;  // scalar elements before / after the body
+    uint64_t trunc_from;  // V_TAIL_TRUNC threshold (element index)
+};
+
+template <typename Tag, int OP, unsigned V>
+__device__ __forceinline__ void reduce2_elem(const R2Args& a, uint64_t idx) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    C acc = widen<Tag>(static_cast<const S*>(a.acc)[idx]);
+    acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in)[idx]), acc);
+    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+}
+
+template <typename Tag, int OP, unsigned V, int U, int B>
+__global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    constexpr int N = 16 / sizeof(S);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head) reduce2_elem<Tag, OP, V>(a, threadIdx.x);
+        if (threadIdx.x < a.tail) reduce2_elem<Tag, OP, V>(a, a.head + a.nvec * N + threadIdx.x);
+    }
+    const size_t hb = (size_t)a.head * sizeof(S);
+    const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.acc) + hb);
+    const u32x4* p1 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in) + hb);
+    u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
+    const uint64_t v0 = (uint64_t)blockIdx.x * (B * U) + threadIdx.x;
+    u32x4 x[U], y[U];
+    const bool full = v0 + (uint64_t)(U - 1) * B < a.nvec;
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        if (full || v0 + (uint64_t)j * B < a.nvec) x[j] = vload<3>(p0 + v0 + (uint64_t)j * B);
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        if (full || v0 + (uint64_t)j * B < a.nvec) y[j] = vload<3>(p1 + v0 + (uint64_t)j * B);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = v0 + (uint64_t)j * B;
+        if (full || v < a.nvec) {
+            Pack<S> px = __builtin_bit_cast(Pack<S>, x[j]), py = __builtin_bit_cast(Pack<S>, y[j]), pr;
+#pragma unroll
+            for (int e = 0; e < N; e++) {
+                const C r = step<Tag, OP, V>(widen<Tag>(py.e[e]), widen<Tag>(px.e[e]));
+                pr.e[e] = finish<Tag, V>(r, a.head + v * N + e, a.trunc_from);
+            }
+            vstore<3>(po + v, __builtin_bit_cast(u32x4, pr));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // element conversions fp32 <-> bf16 / fp16 (ccl_convert_*_arrays,
 // src/comp/bf16/bf16.cpp:113-169, src/comp/fp16/fp16.cpp:55-61)
 // ---------------------------------------------------------------------------

@@ -76,6 +76,23 @@ void add_reduce(std::vector<Variant>& vs, KArgs a, int cap, double traffic) {
                   }, {}});
 }
 
+template <int U, int B>
+void add_reduce2(std::vector<Variant>& vs, KArgs a, double traffic) {
+    R2Args r{};
+    r.acc = a.in[0];
+    r.in = a.in[1];
+    r.out = a.out;
+    r.nvec = a.nvec;
+    r.trunc_from = a.count;
+    const uint64_t blocks = (a.nvec + (uint64_t)B * U - 1) / ((uint64_t)B * U);
+    char name[128];
+    snprintf(name, sizeof name, "reduce2 lean B=%d U=%d grid=%llu", B, U, (unsigned long long)blocks);
+    vs.push_back({name, traffic, [r, blocks](hipStream_t s) {
+                      hipLaunchKernelGGL((reduce2_kernel<float, OP_SUM, 0u, U, B>), dim3((unsigned)blocks), dim3(B),
+                                         0, s, r);
+                  }, {}});
+}
+
 template <int KT, int U, int MAP = 0, int B = kBlock>
 void add_fanin(std::vector<Variant>& vs, KArgs a, double traffic) {
     const uint64_t tile = (uint64_t)B * U;
@@ -116,15 +133,15 @@ int main(int argc, char** argv) {
     const double t3 = 3.0 * bytes;
 
     std::vector<Variant> vs;
-    add_reduce<4, 3, 256>(vs, a, 0, t3);  // the library's configuration
-    add_reduce<1, 3, 256>(vs, a, 0, t3);
-    add_reduce<2, 3, 256>(vs, a, 0, t3);
-    add_reduce<1, 3, 512>(vs, a, 0, t3);
-    add_reduce<2, 3, 512>(vs, a, 0, t3);
-    add_reduce<4, 3, 512>(vs, a, 0, t3);
-    add_reduce<1, 3, 1024>(vs, a, 0, t3);
-    add_reduce<2, 3, 1024>(vs, a, 0, t3);
-    add_reduce<4, 3, 1024>(vs, a, 0, t3);
+    add_reduce<4, 3, 256>(vs, a, 0, t3);  // the general kernel
+    add_reduce2<4, 256>(vs, a, t3);
+    add_reduce2<2, 256>(vs, a, t3);
+    add_reduce2<1, 256>(vs, a, t3);
+    add_reduce2<1, 512>(vs, a, t3);
+    add_reduce2<2, 512>(vs, a, t3);
+    add_reduce2<1, 1024>(vs, a, t3);
+    add_reduce2<2, 1024>(vs, a, t3);
+    add_reduce2<4, 1024>(vs, a, t3);
     // 8-input fan-in (C4): 7 more input buffers, one output
     std::vector<float*> fan(8, nullptr);
     fan[0] = io;
@@ -142,10 +159,6 @@ int main(int argc, char** argv) {
     f8.trunc_from = n;
     const double t9 = 9.0 * bytes;
     add_fanin<0, 4>(vs, f8, t9);
-    add_fanin<0, 1, 0, 1024>(vs, f8, t9);
-    add_fanin<0, 2, 0, 1024>(vs, f8, t9);
-    add_fanin<0, 2, 0, 512>(vs, f8, t9);
-    add_fanin<8, 1, 0, 1024>(vs, f8, t9);
     {
         const uint64_t nvec = bytes / 16;
         const uint64_t blocks = (nvec + kBlock * 4 - 1) / (kBlock * 4);
