@@ -128,12 +128,30 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
 // kernel table
 // ---------------------------------------------------------------------------
 typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
+typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
 
-template <typename Tag, int OP, unsigned V, int KT>
-hipError_t launch_one(dim3 grid, hipStream_t s, const KArgs& a) {
-    hipLaunchKernelGGL((reduce_kernel<Tag, OP, V, KT, kUnroll, kMem>), grid, dim3(kBlock), 0, s, a);
+// Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
+constexpr int kB2 = 256;
+constexpr int kU2 = 4;
+
+template <typename Tag, int OP, unsigned V>
+hipError_t launch_general(dim3 grid, hipStream_t s, const KArgs& a) {
+    hipLaunchKernelGGL((reduce_kernel<Tag, OP, V, 0, kUnroll, kMem>), grid, dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
+
+template <typename Tag, int OP, unsigned V>
+hipError_t launch_lean(dim3 grid, hipStream_t s, const R2Args& a) {
+    hipLaunchKernelGGL((reduce2_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), 0, s, a);
+    return hipGetLastError();
+}
+
+// general: any K (runtime), grid-stride, also the element loop for operands
+// with different misalignments; lean: K = 2 with a common alignment
+struct Kern {
+    LaunchFn general = nullptr;
+    Launch2Fn lean = nullptr;
+};
 
 template <typename Tag, int OP, unsigned V>
 constexpr bool valid_v() {
@@ -147,50 +165,52 @@ constexpr bool valid_v() {
 }
 
 template <typename Tag, int OP, unsigned V>
-LaunchFn entry(bool k2) {
-    if constexpr (valid_v<Tag, OP, V>())
-        return k2 ? &launch_one<Tag, OP, V, 2> : &launch_one<Tag, OP, V, 0>;
-    else
-        return nullptr;
+Kern entry() {
+    Kern k;
+    if constexpr (valid_v<Tag, OP, V>()) {
+        k.general = &launch_general<Tag, OP, V>;
+        k.lean = &launch_lean<Tag, OP, V>;
+    }
+    return k;
 }
 
 template <typename Tag, int OP>
-LaunchFn pick_v(unsigned v, bool k2) {
+Kern pick_v(unsigned v) {
     switch (v) {
-#define MI_V(n) case n: return entry<Tag, OP, n##u>(k2);
+#define MI_V(n) case n: return entry<Tag, OP, n##u>();
         MI_V(0) MI_V(1) MI_V(2) MI_V(3) MI_V(4) MI_V(5) MI_V(6) MI_V(7)
         MI_V(8) MI_V(9) MI_V(10) MI_V(11) MI_V(12) MI_V(13) MI_V(14) MI_V(15)
 #undef MI_V
-        default: return nullptr;
+        default: return Kern();
     }
 }
 
 template <typename Tag>
-LaunchFn pick_op(int op, unsigned v, bool k2) {
+Kern pick_op(int op, unsigned v) {
     switch (op) {
-        case MI_OP_SUM: return pick_v<Tag, OP_SUM>(v, k2);
-        case MI_OP_PROD: return pick_v<Tag, OP_PROD>(v, k2);
-        case MI_OP_MIN: return pick_v<Tag, OP_MIN>(v, k2);
-        case MI_OP_MAX: return pick_v<Tag, OP_MAX>(v, k2);
-        default: return nullptr;
+        case MI_OP_SUM: return pick_v<Tag, OP_SUM>(v);
+        case MI_OP_PROD: return pick_v<Tag, OP_PROD>(v);
+        case MI_OP_MIN: return pick_v<Tag, OP_MIN>(v);
+        case MI_OP_MAX: return pick_v<Tag, OP_MAX>(v);
+        default: return Kern();
     }
 }
 
-LaunchFn pick(int dt, int op, unsigned v, bool k2) {
+Kern pick(int dt, int op, unsigned v) {
     switch (dt) {
-        case MI_INT8: return pick_op<int8_t>(op, v, k2);
-        case MI_UINT8: return pick_op<uint8_t>(op, v, k2);
-        case MI_INT16: return pick_op<int16_t>(op, v, k2);
-        case MI_UINT16: return pick_op<uint16_t>(op, v, k2);
-        case MI_INT32: return pick_op<int32_t>(op, v, k2);
-        case MI_UINT32: return pick_op<uint32_t>(op, v, k2);
-        case MI_INT64: return pick_op<int64_t>(op, v, k2);
-        case MI_UINT64: return pick_op<uint64_t>(op, v, k2);
-        case MI_FLOAT16: return pick_op<fp16_tag>(op, v, k2);
-        case MI_FLOAT32: return pick_op<float>(op, v, k2);
-        case MI_FLOAT64: return pick_op<double>(op, v, k2);
-        case MI_BFLOAT16: return pick_op<bf16_tag>(op, v, k2);
-        default: return nullptr;
+        case MI_INT8: return pick_op<int8_t>(op, v);
+        case MI_UINT8: return pick_op<uint8_t>(op, v);
+        case MI_INT16: return pick_op<int16_t>(op, v);
+        case MI_UINT16: return pick_op<uint16_t>(op, v);
+        case MI_INT32: return pick_op<int32_t>(op, v);
+        case MI_UINT32: return pick_op<uint32_t>(op, v);
+        case MI_INT64: return pick_op<int64_t>(op, v);
+        case MI_UINT64: return pick_op<uint64_t>(op, v);
+        case MI_FLOAT16: return pick_op<fp16_tag>(op, v);
+        case MI_FLOAT32: return pick_op<float>(op, v);
+        case MI_FLOAT64: return pick_op<double>(op, v);
+        case MI_BFLOAT16: return pick_op<bf16_tag>(op, v);
+        default: return Kern();
     }
 }
 
@@ -213,41 +233,60 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         if (out != inputs[0]) MI_HIP(hipMemcpyAsync(out, inputs[0], count * es, hipMemcpyDeviceToDevice, stream));
         return 0;
     }
-    LaunchFn fn = pick(dt, op, v, k == 2);
-    if (!fn) return fail(MI_E_UNSUPPORTED, "no kernel for this dtype/op/variant");
-
-    KArgs a;
-    memset(&a, 0, sizeof(a));
-    for (int i = 0; i < k; i++) a.in[i] = inputs[i];
-    a.out = out;
-    a.k = k;
-    a.count = count;
+    const Kern kern = pick(dt, op, v);
+    if (!kern.general) return fail(MI_E_UNSUPPORTED, "no kernel for this dtype/op/variant");
     // VCVTNEPS2BF16 main part / scalar tail split of ccl_convert_fp32_to_bf16_arrays
-    a.trunc_from = (count / 16) * 16;
+    const uint64_t trunc_from = (count / 16) * 16;
 
-    // common misalignment -> scalar head; different misalignments -> scalar loop
+    // common misalignment -> scalar head + vector body + scalar tail;
+    // different misalignments -> element loop (general kernel)
     const uintptr_t mis = reinterpret_cast<uintptr_t>(out) & 15u;
     bool same = (mis % es) == 0;
     for (int i = 0; i < k && same; i++) same = ((reinterpret_cast<uintptr_t>(inputs[i]) & 15u) == mis);
     const size_t n_per_vec = 16 / es;
-    uint64_t blocks;
-    if (same) {
-        const size_t head = mis ? std::min<size_t>((16 - mis) / es, count) : 0;
-        const size_t body = count - head;
-        a.head = head;
-        a.nvec = body / n_per_vec;
-        a.tail = body - a.nvec * n_per_vec;
-        const uint64_t tile = (uint64_t)kBlock * kUnroll;
-        blocks = (a.nvec + tile - 1) / tile;
-        const int cap = max_blocks();
-        if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
-        if (blocks == 0) blocks = 1;
+    const size_t head = same && mis ? std::min<size_t>((16 - mis) / es, count) : 0;
+    const uint64_t nvec = same ? (count - head) / n_per_vec : 0;
+    const size_t tail = same ? count - head - nvec * n_per_vec : 0;
+
+    hipError_t e;
+    if (same && k == 2) {
+        R2Args r;
+        r.acc = inputs[0];
+        r.in = inputs[1];
+        r.out = out;
+        r.nvec = nvec;
+        r.head = (uint32_t)head;
+        r.tail = (uint32_t)tail;
+        r.trunc_from = trunc_from;
+        const uint64_t tile = (uint64_t)kB2 * kU2;
+        uint64_t blocks = std::max<uint64_t>((nvec + tile - 1) / tile, 1);
+        if (blocks > 0x7FFFFFFFull) return fail(MI_E_UNSUPPORTED, "bucket too large for one launch");
+        e = kern.lean(dim3((unsigned)blocks), stream, r);
     } else {
-        a.scalar_only = 1;
-        blocks = std::min<uint64_t>((count + kBlock - 1) / kBlock, 8192);
+        KArgs a;
+        memset(&a, 0, sizeof(a));
+        for (int i = 0; i < k; i++) a.in[i] = inputs[i];
+        a.out = out;
+        a.k = k;
+        a.count = count;
+        a.trunc_from = trunc_from;
+        uint64_t blocks;
+        if (same) {
+            a.head = head;
+            a.nvec = nvec;
+            a.tail = tail;
+            const uint64_t tile = (uint64_t)kBlock * kUnroll;
+            blocks = (a.nvec + tile - 1) / tile;
+            const int cap = max_blocks();
+            if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
+            if (blocks == 0) blocks = 1;
+        } else {
+            a.scalar_only = 1;
+            blocks = std::min<uint64_t>((count + kBlock - 1) / kBlock, 8192);
+        }
+        if (blocks > 0x7FFFFFFFull) blocks = 0x7FFFFFFFull;  // grid-stride covers the rest
+        e = kern.general(dim3((unsigned)blocks), stream, a);
     }
-    if (blocks > 0x7FFFFFFFull) blocks = 0x7FFFFFFFull;
-    hipError_t e = fn(dim3((unsigned)blocks), stream, a);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;
 }
