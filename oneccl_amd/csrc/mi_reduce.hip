@@ -131,8 +131,8 @@ typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
 typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
 
 // Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
-constexpr int kB2 = 256;
-constexpr int kU2 = 4;
+constexpr int kB2 = 1024;
+constexpr int kU2 = 1;
 
 template <typename Tag, int OP, unsigned V>
 hipError_t launch_general(dim3 grid, hipStream_t s, const KArgs& a) {
