@@ -407,6 +407,73 @@ __global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// Lean K-input fan-in (compile-time K): one tile of B*U vectors per block,
+// every input's loads issued before the first combine, left fold in the
+// reference's order (acc = in[0]; acc = op(in[j], acc)).  Requires a common
+// alignment; head/tail by block 0.
+// ---------------------------------------------------------------------------
+struct RKArgs {
+    const void* in[kMaxInputs];
+    void* out;
+    uint64_t nvec;
+    uint32_t head, tail;
+    uint64_t trunc_from;
+};
+
+template <typename Tag, int OP, unsigned V, int K>
+__device__ __forceinline__ void reducek_elem(const RKArgs& a, uint64_t idx) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
+#pragma unroll
+    for (int i = 1; i < K; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
+    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+}
+
+template <typename Tag, int OP, unsigned V, int K, int U, int B>
+__global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    constexpr int N = 16 / sizeof(S);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head) reducek_elem<Tag, OP, V, K>(a, threadIdx.x);
+        if (threadIdx.x < a.tail) reducek_elem<Tag, OP, V, K>(a, a.head + a.nvec * N + threadIdx.x);
+    }
+    const size_t hb = (size_t)a.head * sizeof(S);
+    const uint64_t v0 = (uint64_t)blockIdx.x * (B * U) + threadIdx.x;
+    const bool full = v0 + (uint64_t)(U - 1) * B < a.nvec;
+    u32x4 x[K][U];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[i]) + hb);
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (full || v0 + (uint64_t)j * B < a.nvec) x[i][j] = vload<3>(p + v0 + (uint64_t)j * B);
+    }
+    u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const uint64_t v = v0 + (uint64_t)j * B;
+        if (full || v < a.nvec) {
+            C acc[N];
+            Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0][j]);
+#pragma unroll
+            for (int e = 0; e < N; e++) acc[e] = widen<Tag>(p0.e[e]);
+#pragma unroll
+            for (int i = 1; i < K; i++) {
+                Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i][j]);
+#pragma unroll
+                for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V>(widen<Tag>(pi.e[e]), acc[e]);
+            }
+            Pack<S> pr;
+#pragma unroll
+            for (int e = 0; e < N; e++) pr.e[e] = finish<Tag, V>(acc[e], a.head + v * N + e, a.trunc_from);
+            vstore<3>(po + v, __builtin_bit_cast(u32x4, pr));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // element conversions fp32 <-> bf16 / fp16 (ccl_convert_*_arrays,
 // src/comp/bf16/bf16.cpp:113-169, src/comp/fp16/fp16.cpp:55-61)
 // ---------------------------------------------------------------------------

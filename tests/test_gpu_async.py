@@ -110,3 +110,39 @@ def test_sharded_in_process(nshards):
     _lib.check(m.mi_reduce_sharded(nshards, (ctypes.c_int * nshards)(*devs), _lib.void_ptr_array(ptrs), k,
                                    _lib.void_ptr_array(outs), (ctypes.c_size_t * nshards)(*counts), FP32, 0, 0))
     assert_same(from_dev(out_t, ins[0]), exp, FP32)
+
+
+def test_hipgraph_capture_and_replay():
+    """The asynchronous entry points do no allocation or synchronisation while
+    launching (cdna_hip_programming.md Guideline 9), so they can be captured
+    into a hipGraph and replayed — e.g. a whole bucket schedule as one graph."""
+    import torch
+    m = _lib.mi()
+    n = 1_000_003
+    a = rand_array(FP32, n, seed=71, specials=False)
+    b = rand_array(FP32, n, seed=72, specials=False)
+    c = rand_array(BF16, n, seed=73, specials=False)
+    d = rand_array(BF16, n, seed=74, specials=False)
+    ta, pa = to_dev(a)
+    tb, pb = to_dev(b)
+    tc, pc = to_dev(c)
+    td, pd = to_dev(d)
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        h = torch.cuda.current_stream().cuda_stream
+        _lib.check(m.mi_reduce(pa, pb, n, FP32, 0, 0, h))
+        _lib.check(m.mi_reduce(pc, pd, n, BF16, 0, 0x3, h))
+    exp_b, exp_d = b.copy(), d.copy()
+    replays = 3
+    for _ in range(replays):
+        oracle.comp_reduce(a, exp_b, FP32, 0)
+        oracle.comp_reduce(c, exp_d, BF16, 0, oracle.BF16_AVX512BF)
+    tb.copy_(to_dev(b)[0])  # capture does not execute; start from the inputs
+    td.copy_(to_dev(d)[0])
+    torch.cuda.synchronize()
+    for _ in range(replays):
+        g.replay()
+    torch.cuda.synchronize()
+    assert_same(from_dev(tb, b), exp_b, FP32)
+    assert_same(from_dev(td, d), exp_d, BF16)

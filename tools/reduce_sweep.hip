@@ -93,6 +93,22 @@ void add_reduce2(std::vector<Variant>& vs, KArgs a, double traffic) {
                   }, {}});
 }
 
+template <int K, int U, int B>
+void add_fanin_lean(std::vector<Variant>& vs, KArgs a, double traffic) {
+    RKArgs r{};
+    for (int i = 0; i < K; i++) r.in[i] = a.in[i];
+    r.out = a.out;
+    r.nvec = a.nvec;
+    r.trunc_from = a.count;
+    const uint64_t blocks = (a.nvec + (uint64_t)B * U - 1) / ((uint64_t)B * U);
+    char name[128];
+    snprintf(name, sizeof name, "fanin lean K=%d B=%d U=%d grid=%llu", K, B, U, (unsigned long long)blocks);
+    vs.push_back({name, traffic, [r, blocks](hipStream_t s) {
+                      hipLaunchKernelGGL((reducek_kernel<float, OP_SUM, 0u, K, U, B>), dim3((unsigned)blocks),
+                                         dim3(B), 0, s, r);
+                  }, {}});
+}
+
 template <int KT, int U, int MAP = 0, int B = kBlock>
 void add_fanin(std::vector<Variant>& vs, KArgs a, double traffic) {
     const uint64_t tile = (uint64_t)B * U;
@@ -134,14 +150,8 @@ int main(int argc, char** argv) {
 
     std::vector<Variant> vs;
     add_reduce<4, 3, 256>(vs, a, 0, t3);  // the general kernel
-    add_reduce2<4, 256>(vs, a, t3);
-    add_reduce2<2, 256>(vs, a, t3);
-    add_reduce2<1, 256>(vs, a, t3);
+    add_reduce2<1, 1024>(vs, a, t3);      // the library's 2-input kernel
     add_reduce2<1, 512>(vs, a, t3);
-    add_reduce2<2, 512>(vs, a, t3);
-    add_reduce2<1, 1024>(vs, a, t3);
-    add_reduce2<2, 1024>(vs, a, t3);
-    add_reduce2<4, 1024>(vs, a, t3);
     // 8-input fan-in (C4): 7 more input buffers, one output
     std::vector<float*> fan(8, nullptr);
     fan[0] = io;
@@ -159,6 +169,12 @@ int main(int argc, char** argv) {
     f8.trunc_from = n;
     const double t9 = 9.0 * bytes;
     add_fanin<0, 4>(vs, f8, t9);
+    add_fanin_lean<8, 1, 1024>(vs, f8, t9);
+    add_fanin_lean<8, 1, 512>(vs, f8, t9);
+    add_fanin_lean<8, 1, 256>(vs, f8, t9);
+    add_fanin_lean<8, 2, 256>(vs, f8, t9);
+    add_fanin_lean<8, 2, 512>(vs, f8, t9);
+    add_fanin_lean<4, 1, 1024>(vs, f8, 5.0 * bytes);
     {
         const uint64_t nvec = bytes / 16;
         const uint64_t blocks = (nvec + kBlock * 4 - 1) / (kBlock * 4);
