@@ -85,6 +85,33 @@ def build_dropin_caller(force: bool = False) -> Path:
     return out
 
 
+def build_asan(force: bool = False) -> Path:
+    """Host-AddressSanitizer builds of the product's host code (device code is
+    not instrumented: GPU ASan is not available on this pool) plus the C++
+    drop-in caller linked against them: lib/asan/*.so, tests/cpp/dropin_caller_asan.
+    Run it with ASAN_OPTIONS=detect_leaks=0 (the HIP runtime keeps its allocations)."""
+    adir = LIB / "asan"
+    adir.mkdir(parents=True, exist_ok=True)
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+    mi = adir / "libmi_reduce.so"
+    if force or _stale(mi, [CSRC / "mi_reduce.hip", CSRC / "reduce_kernels.hpp"]):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", *san,
+              "-o", str(mi), str(CSRC / "mi_reduce.hip")])
+    shim = adir / "libccl_comp_hip.so"
+    if force or _stale(shim, [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", mi]):
+        _run([os.environ.get("CXX", "g++"), "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-fsanitize=address",
+              "-fno-omit-frame-pointer", "-o", str(shim), str(CSRC / "comp.cpp"), f"-L{adir}", "-lmi_reduce",
+              "-Wl,-rpath,$ORIGIN"])
+    src = ROOT / "tests" / "cpp" / "dropin_caller.cpp"
+    out = ROOT / "tests" / "cpp" / "dropin_caller_asan"
+    if force or _stale(out, [src, shim]):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", *san, "-fsanitize=address", "-o",
+              str(out), str(src),
+              f"-L{adir}", "-lccl_comp_hip", "-lmi_reduce", f"-Wl,-rpath,{adir}",
+              "-Wl,-rpath,$ORIGIN/../../oneccl_amd/lib/asan"])
+    return out
+
+
 def build_oracle(force: bool = False) -> Path:
     """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile)."""
     odir = ROOT / "oracle"

@@ -102,6 +102,71 @@ int main() {
     }
     EXPECT(threw, "custom without fn must throw (comp.cpp:85)");
 
+    // large pageable host buffers: more than one 32 MiB staging chunk, odd count
+    {
+        const size_t m = (80u << 20) / 4 + 5;
+        float* x = static_cast<float*>(staging_alloc(m * 4));
+        float* y = static_cast<float*>(staging_alloc(m * 4));
+        for (size_t i = 0; i < m; i++) {
+            x[i] = (float)(i % 97);
+            y[i] = 1.0f;
+        }
+        ccl_comp_reduce(nullptr, x, m, y, nullptr, f32, ccl::reduction::sum, nullptr, nullptr);
+        bool okk = true;
+        for (size_t i = 0; i < m; i++) okk = okk && y[i] == (float)(i % 97) + 1.0f;
+        EXPECT(okk, "pageable multi-chunk");
+        // misaligned sub-buffers (ring chunks at odd element offsets)
+        ccl_comp_reduce(nullptr, x + 1, m - 3, y + 3, nullptr, f32, ccl::reduction::max, nullptr, nullptr);
+        // pinned host buffers: zero-copy kernel path
+        float *px = nullptr, *py = nullptr;
+        if (hipHostMalloc(&px, m * 4, 0) == hipSuccess && hipHostMalloc(&py, m * 4, 0) == hipSuccess) {
+            memcpy(px, x, m * 4);
+            for (size_t i = 0; i < m; i++) py[i] = 2.0f;
+            ccl_comp_reduce(nullptr, px, m, py, nullptr, f32, ccl::reduction::prod, nullptr, nullptr);
+            okk = true;
+            for (size_t i = 0; i < m; i++) okk = okk && py[i] == 2.0f * x[i];
+            EXPECT(okk, "pinned zero-copy");
+            (void)hipHostFree(px);
+            (void)hipHostFree(py);
+        }
+        free(x);
+        free(y);
+    }
+
+    // batch reduce with more inputs than one fused launch takes (chained groups)
+    {
+        const size_t k = 23, m = 1001;
+        std::vector<float> pk(k * m);
+        for (size_t j = 0; j < k; j++)
+            for (size_t i = 0; i < m; i++) pk[j * m + i] = 1.0f;
+        std::vector<float> out(pk.begin(), pk.begin() + m);
+        std::vector<size_t> offs(k);
+        for (size_t j = 0; j < k; j++) offs[j] = j * m;
+        ccl_comp_batch_reduce(pk.data(), offs, m, out.data(), nullptr, f32, ccl::reduction::sum, nullptr, nullptr, 0,
+                              nullptr, nullptr);
+        EXPECT(out[0] == 23.0f && out[m - 1] == 23.0f, "batch k=23: %f", out[0]);
+        // bf16 keep-precision (fp32 accumulate, one rounding)
+        std::vector<uint16_t> bk(4 * 33, 0x3F80);  // 1.0
+        std::vector<uint16_t> bo(bk.begin(), bk.begin() + 33);
+        std::vector<size_t> o4 = {0, 33, 66, 99};
+        ccl_comp_batch_reduce(bk.data(), o4, 33, bo.data(), nullptr, ccl_datatype(ccl::datatype::bfloat16, 2),
+                              ccl::reduction::sum, nullptr, nullptr, 1, nullptr, nullptr);
+        EXPECT(bo[0] == 0x4080 && bo[32] == 0x4080, "keep precision 4.0 = %04x", bo[0]);
+    }
+
+    // conversions with a count%16 tail
+    {
+        std::vector<float> f(37);
+        for (size_t i = 0; i < f.size(); i++) f[i] = 1.0f + (float)i / 3.0f;
+        std::vector<uint16_t> h(37);
+        ccl_convert_fp32_to_bf16_arrays(f.data(), h.data(), h.size());
+        std::vector<float> back(37);
+        ccl_convert_bf16_to_fp32_arrays(h.data(), back.data(), back.size());
+        bool okk = true;
+        for (size_t i = 0; i < f.size(); i++) okk = okk && std::fabs(back[i] - f[i]) <= f[i] / 64;
+        EXPECT(okk, "bf16 arrays round trip");
+    }
+
     free(comm_buf);
     free(acc);
     (void)hipFree(din);

@@ -306,3 +306,21 @@ def test_cpp_caller_links_dropin_by_mangled_names():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin_caller: ok" in r.stdout
+
+
+def test_cpp_caller_under_host_asan():
+    """Host AddressSanitizer over the product's host code (staging pipeline,
+    zero-copy, fan-in chaining, conversions): the drop-in caller linked
+    against -Xarch_host -fsanitize=address builds of both libraries.  Device
+    code is not instrumented (GPU ASan is not available on this pool)."""
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent / "cpp" / "dropin_caller_asan"
+    if not exe.exists():
+        from oneccl_amd import build
+        build.build_asan()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "dropin_caller: ok" in r.stdout

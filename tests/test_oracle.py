@@ -193,3 +193,14 @@ def test_int_wrap_and_minmax():
         x = b.copy()
         oracle.comp_reduce(a, x, 0, op)
         assert x.tolist() == exp, OP_NAME[op]
+
+
+def test_oracle_is_sanitizer_clean():
+    """The restatement under AddressSanitizer + UndefinedBehaviorSanitizer
+    (oracle/selftest.c over every entry point, odd sizes, all impls)."""
+    r = subprocess.run(["make", "-C", str(ROOT / "oracle"), "asan"], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("no sanitizer runtime for this compiler: " + r.stderr[-200:])
+    r = subprocess.run([str(ROOT / "oracle" / "lib" / "selftest_asan")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "selftest: ok" in r.stdout

@@ -29,6 +29,8 @@ for step in "$@"; do
             run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider ;;
         tests_fast)
             run pytest_gpu 600 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider -k "not full" ;;
+        asan)
+            ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 run asan 300 ./tests/cpp/dropin_caller_asan ;;
         smoke)
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         sweep)
