@@ -99,7 +99,10 @@ def build_asan(force: bool = False) -> Path:
               "-o", str(mi), str(CSRC / "mi_reduce.hip")])
     shim = adir / "libccl_comp_hip.so"
     if force or _stale(shim, [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", mi]):
-        _run([os.environ.get("CXX", "g++"), "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-fsanitize=address",
+        # the same compiler (and so the same ASan runtime) as the hipcc-built pieces
+        clang = next((c for c in ("/opt/rocm/lib/llvm/bin/clang++", "/opt/rocm/llvm/bin/clang++")
+                      if Path(c).exists()), "clang++")
+        _run([clang, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-fsanitize=address",
               "-fno-omit-frame-pointer", "-o", str(shim), str(CSRC / "comp.cpp"), f"-L{adir}", "-lmi_reduce",
               "-Wl,-rpath,$ORIGIN"])
     src = ROOT / "tests" / "cpp" / "dropin_caller.cpp"
