@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's work")
     p.add_argument("--no-host-leg", action="store_true", help="skip the host-resident (PCIe) measurement")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
+                        "one GPU when rehearsing the N>1 path)")
     return p.parse_args()
 
 
@@ -171,9 +174,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local_rank % max(ndev, 1))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     cfg = CONFIGS[args.config]
     desc, dt, es, op, k, bucket, flags = cfg
@@ -224,7 +232,7 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     avg_kern_ms = statistics.mean(kern_ms)
 
-    elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, "cuda")
+    elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, coll_dev)
 
     units_per_rank = n * es  # bucket bytes this rank reduced per step
     value = total_bytes * args.steps / elapsed / GiB

@@ -129,6 +129,7 @@ def build_all(force: bool = False) -> None:
     build_shim(force)
     build_sweep(force)
     build_dropin_caller(force)
+    build_asan(force)
     build_oracle(force)
 
 

@@ -45,6 +45,11 @@ for step in "$@"; do
             run c1_dropin_p4 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 &&
             run c1_dropin_p4_fused 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 --fused &&
             run c1_oracle_p4 300 python tools/c1_allreduce.py --reduce oracle --ranks 4 ;;
+        dist2)
+            run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo &&
+            run dist2_strong 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                --master-port 29534 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --scaling strong ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
         benchall)
