@@ -73,6 +73,15 @@ def build_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_latency(force: bool = False) -> Path:
+    out = ROOT / "tools" / "latency"
+    src = ROOT / "tools" / "latency.hip"
+    if src.exists() and (force or _stale(out, [src, LIB / "libmi_reduce.so"])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-Wno-unused-result", "-o", str(out), str(src),
+              f"-L{LIB}", "-lmi_reduce", "-Wl,-rpath,$ORIGIN/../oneccl_amd/lib"])
+    return out
+
+
 def build_dropin_caller(force: bool = False) -> Path:
     """Test program: a C++ caller linking libccl_comp_hip.so by oneCCL's own
     mangled names (tests/cpp/dropin_caller.cpp)."""
@@ -128,6 +137,7 @@ def build_all(force: bool = False) -> None:
     build_mi_reduce(force)
     build_shim(force)
     build_sweep(force)
+    build_latency(force)
     build_dropin_caller(force)
     build_asan(force)
     build_oracle(force)

@@ -31,6 +31,8 @@ for step in "$@"; do
             run pytest_gpu 600 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider -k "not full" ;;
         asan)
             ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 run asan 300 ./tests/cpp/dropin_caller_asan ;;
+        latency)
+            run latency 300 ./tools/latency 2000 ;;
         smoke)
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         sweep)

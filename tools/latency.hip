@@ -1,0 +1,74 @@
+// latency.hip — where the synchronous small-bucket call spends its time.
+// Host wall-clock (steady_clock), min and median over many reps, one JSON
+// line per item.  Links libmi_reduce.so.
+//   latency [reps=2000]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <vector>
+
+#include "../include/mi_reduce.h"
+
+__global__ void empty_kernel() {}
+
+static void measure(const char* name, int reps, const std::function<void()>& f) {
+    std::vector<double> t(reps);
+    for (int i = 0; i < 50; i++) f();
+    for (int i = 0; i < reps; i++) {
+        auto t0 = std::chrono::steady_clock::now();
+        f();
+        auto t1 = std::chrono::steady_clock::now();
+        t[i] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    }
+    std::sort(t.begin(), t.end());
+    printf("{\"item\": \"%s\", \"min_us\": %.2f, \"median_us\": %.2f, \"p90_us\": %.2f}\n", name, t[0],
+           t[reps / 2], t[reps * 9 / 10]);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 2000;
+    const size_t n = 1024;  // 4 KiB fp32
+    float *a, *b, *ha, *hb;
+    hipMalloc(&a, n * 4);
+    hipMalloc(&b, n * 4);
+    hipMemset(a, 0, n * 4);
+    hipMemset(b, 0, n * 4);
+    hipHostMalloc(&ha, n * 4, 0);
+    hipHostMalloc(&hb, n * 4, 0);
+    std::vector<float> pa(n, 1.f), pb(n, 1.f);
+    hipStream_t s;
+    hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    hipPointerAttribute_t at;
+    int dev = 0;
+
+    measure("empty kernel launch (host side only)", reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s); });
+    hipStreamSynchronize(s);
+    measure("empty kernel launch + hipStreamSynchronize", reps, [&] {
+        hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
+        hipStreamSynchronize(s);
+    });
+    measure("hipPointerGetAttributes (device ptr)", reps, [&] { hipPointerGetAttributes(&at, a); });
+    measure("hipPointerGetAttributes (pageable ptr)", reps, [&] {
+        if (hipPointerGetAttributes(&at, pa.data()) != hipSuccess) (void)hipGetLastError();
+    });
+    measure("hipGetDevice + hipSetDevice", reps, [&] {
+        hipGetDevice(&dev);
+        hipSetDevice(dev);
+    });
+    measure("mi_reduce 4 KiB (async launch, host side)", reps, [&] { mi_reduce(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, s); });
+    hipStreamSynchronize(s);
+    measure("mi_reduce 4 KiB + hipStreamSynchronize", reps, [&] {
+        mi_reduce(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, s);
+        hipStreamSynchronize(s);
+    });
+    measure("mi_reduce_sync 4 KiB device", reps, [&] { mi_reduce_sync(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
+    measure("mi_reduce_sync 4 KiB pinned host (zero-copy)", reps, [&] { mi_reduce_sync(ha, hb, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
+    measure("mi_reduce_sync 4 KiB pageable host (staged)", reps / 4,
+            [&] { mi_reduce_sync(pa.data(), pb.data(), n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
+    return 0;
+}
