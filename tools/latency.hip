@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../include/mi_reduce.h"
+#include "../oneccl_amd/csrc/reduce_kernels.hpp"
 
 __global__ void empty_kernel() {}
 
@@ -60,6 +61,22 @@ int main(int argc, char** argv) {
         hipGetDevice(&dev);
         hipSetDevice(dev);
     });
+    mi::R2Args r{};
+    r.acc = b;
+    r.in = a;
+    r.out = b;
+    r.nvec = n / 4;
+    r.trunc_from = n;
+    measure("reduce2_kernel direct hipLaunchKernelGGL (host side)", reps, [&] {
+        hipLaunchKernelGGL((mi::reduce2_kernel<float, 0, 0u, 1, 1024>), dim3(1), dim3(1024), 0, s, r);
+    });
+    hipStreamSynchronize(s);
+    measure("reduce2_kernel direct launch + hipGetLastError", reps, [&] {
+        hipLaunchKernelGGL((mi::reduce2_kernel<float, 0, 0u, 1, 1024>), dim3(1), dim3(1024), 0, s, r);
+        (void)hipGetLastError();
+    });
+    hipStreamSynchronize(s);
+    measure("hipGetLastError alone", reps, [&] { (void)hipGetLastError(); });
     measure("mi_reduce 4 KiB (async launch, host side)", reps, [&] { mi_reduce(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, s); });
     hipStreamSynchronize(s);
     measure("mi_reduce 4 KiB + hipStreamSynchronize", reps, [&] {
