@@ -239,6 +239,22 @@ def main():
     traffic_per_launch = (k + 1) * n * es  # read k inputs, write 1 (algorithmic)
     achieved = traffic_per_launch / (avg_kern_ms / 1e3) / 1e9
 
+    # the same bucket through oneCCL's own entry point: ccl_comp_reduce of the
+    # drop-in shim (synchronous, as src/sched calls it) — reported beside `value`
+    dropin = None
+    if k == 2:
+        shim = _lib.shim()
+        torch.cuda.synchronize()
+        tt = []
+        for _ in range(max(3, min(10, args.steps))):
+            t0 = time.perf_counter()
+            rc = shim.mi_ccl_comp_reduce(ins[1].data_ptr(), n, ins[0].data_ptr(), None, dt, op)
+            tt.append(time.perf_counter() - t0)
+            _lib.check_shim(rc, "ccl_comp_reduce")
+        dropin = {"value": round(n * es / GiB / statistics.median(tt), 2), "unit": "GiB/s",
+                  "best": round(n * es / GiB / min(tt), 2), "calls": len(tt),
+                  "entry": "ccl_comp_reduce (libccl_comp_hip.so, synchronous, oneCCL's C++ signature)"}
+
     host_leg = None
     if rank == 0 and world == 1 and not args.no_host_leg and k == 2:
         host_leg = host_resident_leg(m, dt, es, op, flags, min(n, (256 << 20) // es))
@@ -277,6 +293,8 @@ def main():
                          "traffic_source": traffic.get("source") if traffic else None},
             "cpu_baseline": cpu,
         }
+        if dropin:
+            out["dropin_sync"] = dropin
         if host_leg:
             out["host_resident"] = host_leg
         print(json.dumps(out), flush=True)
