@@ -394,16 +394,29 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     PtrKind kin[MI_MAX_INPUTS];
     const void* dins[MI_MAX_INPUTS];
     int pdev = -1;
-    bool all_dev = true;
+    bool all_dev = true, mixed_dev = false;
     for (int i = 0; i < k; i++) {
         void* dp = const_cast<void*>(inputs[i]);
-        kin[i] = classify(inputs[i], &pdev, &dp);
+        int d_i = -1;
+        kin[i] = classify(inputs[i], &d_i, &dp);
         dins[i] = dp;
         all_dev = all_dev && kin[i] == PK_DEVICE;
+        if (d_i >= 0) {
+            mixed_dev = mixed_dev || (pdev >= 0 && d_i != pdev);
+            pdev = d_i;
+        }
     }
     void* dout = out;
-    const PtrKind kout = classify(out, &pdev, &dout);
+    int d_o = -1;
+    const PtrKind kout = classify(out, &d_o, &dout);
     all_dev = all_dev && kout == PK_DEVICE;
+    if (d_o >= 0) {
+        mixed_dev = mixed_dev || (pdev >= 0 && d_o != pdev);
+        pdev = d_o;
+    }
+    // one kernel reads every operand: operands on two GPUs would need peer
+    // access the caller never set up — refuse instead of faulting
+    if (mixed_dev) return fail(MI_E_UNSUPPORTED, "device operands live on different GPUs");
     if (device < 0 && pdev >= 0) device = pdev;
 
     DevCtx* d = nullptr;
