@@ -310,7 +310,8 @@ def host_resident_leg(m, dt, es, op, flags, n):
     import torch
     res = {}
     nbytes = n * es
-    for kind in ("pinned", "pinned_staged", "pageable"):
+    reg_s = None
+    for kind in ("pinned", "pinned_staged", "pageable", "pageable_registered"):
         m.mi_set_host_mode(1 if kind == "pinned_staged" else 0)
         if kind.startswith("pinned"):
             a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -320,6 +321,11 @@ def host_resident_leg(m, dt, es, op, flags, n):
             a = np.zeros(nbytes, np.uint8)
             b = np.zeros(nbytes, np.uint8)
             pa, pb = a.ctypes.data, b.ctypes.data
+            if kind == "pageable_registered":  # what oneCCL's buffer cache would do once per buffer
+                t0 = time.perf_counter()
+                m.mi_host_register(pa, nbytes)
+                m.mi_host_register(pb, nbytes)
+                reg_s = time.perf_counter() - t0
         m.mi_reduce_sync(pa, pb, n, dt, op, flags, -1)  # warm: staging buffers, page faults
         times = []
         for _ in range(5):
@@ -329,11 +335,16 @@ def host_resident_leg(m, dt, es, op, flags, n):
             if rc:
                 return {"error": m.mi_last_error().decode()}
         res[kind] = round(nbytes / GiB / min(times), 3)
+        if kind == "pageable_registered":
+            m.mi_host_unregister(pa)
+            m.mi_host_unregister(pb)
     m.mi_set_host_mode(0)
+    res["register_ms_two_buffers"] = round(reg_s * 1e3, 2) if reg_s is not None else None
     return {"unit": "GiB/s bucket incl. both operands host->GPU and the result GPU->host over PCIe",
             "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync",
             "modes": "pinned = zero-copy kernel on pinned host memory (default); pinned_staged = chunked "
-                     "H2D/kernel/D2H over two streams; pageable = staged"}
+                     "H2D/kernel/D2H over two streams; pageable = staged; pageable_registered = pageable buffers "
+                     "registered once with mi_host_register (cost in register_ms_two_buffers), then zero-copy"}
 
 
 def pmc_traffic(config):

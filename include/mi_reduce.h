@@ -196,6 +196,17 @@ int mi_shard_range(size_t count, int rank, int world, size_t align,
  * sycl::get_pointer_type for (src/comp/comp.cpp:145-147).                 */
 int mi_pointer_kind(const void* ptr, int* device);
 
+/* ---- staging-buffer registration ------------------------------------- *
+ * Pin (page-lock and map for every GPU) an existing pageable host buffer, so
+ * later mi_*_sync calls on it take the zero-copy path instead of staging.
+ * Meant for buffers that live long: oneCCL's regular_buffer_cache reuses its
+ * staging buffers and already registers them with Level Zero at this point
+ * (src/sched/buffer/buffer_cache.cpp:99-104, import_external_pointer);
+ * INTEGRATION.md shows the two-line HIP equivalent.  mi_host_unregister must
+ * run before the memory is freed.                                          */
+int mi_host_register(void* ptr, size_t bytes);
+int mi_host_unregister(void* ptr);
+
 /* ---- host-operand strategy ------------------------------------------- *
  * How mi_*_sync treats host operands.  MI_HOST_AUTO (default): pinned host
  * memory is read and written in place by the kernel over PCIe (zero-copy,

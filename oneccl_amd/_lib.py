@@ -50,6 +50,8 @@ MI_API = [
     ("mi_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("mi_shard_range", c_int, [c_size_t, c_int, c_int, c_size_t, POINTER(c_size_t), POINTER(c_size_t)]),
     ("mi_pointer_kind", c_int, [c_void_p, POINTER(c_int)]),
+    ("mi_host_register", c_int, [c_void_p, c_size_t]),
+    ("mi_host_unregister", c_int, [c_void_p]),
     ("mi_reduction_to_str", c_char_p, [c_int]),
     ("mi_dtype_size", c_size_t, [c_int]),
     ("mi_last_error", c_char_p, []),

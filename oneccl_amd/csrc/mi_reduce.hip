@@ -830,6 +830,18 @@ const char* mi_reduction_to_str(int op) {
     }
 }
 
+int mi_host_register(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return fail(MI_E_INVALID, "null / empty buffer");
+    MI_HIP(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    return 0;
+}
+
+int mi_host_unregister(void* ptr) {
+    if (!ptr) return fail(MI_E_INVALID, "null buffer");
+    MI_HIP(hipHostUnregister(ptr));
+    return 0;
+}
+
 int mi_pointer_kind(const void* ptr, int* device) {
     int dev = -1;
     const int kind = (int)classify(ptr, &dev);

@@ -324,3 +324,32 @@ def test_cpp_caller_under_host_asan():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "dropin_caller: ok" in r.stdout
+
+
+@pytest.mark.parametrize("dt", [FP32, BF16])
+def test_registered_staging_buffer_takes_zero_copy(dt):
+    """A pageable staging buffer registered once (what oneCCL's buffer cache
+    would do) is classified pinned and reduced in place."""
+    import time
+    m = _lib.mi()
+    n = (64 << 20) // 4 + 3
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=81, specials=False)
+    b = rand_array(dt, n, seed=82, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+    dev = ctypes.c_int(-1)
+    assert m.mi_pointer_kind(ptr(b), ctypes.byref(dev)) == 2  # pageable
+    t0 = time.perf_counter()
+    _lib.check(m.mi_host_register(ptr(a), a.nbytes))
+    _lib.check(m.mi_host_register(ptr(b), b.nbytes))
+    t_reg = time.perf_counter() - t0
+    try:
+        assert m.mi_pointer_kind(ptr(b), ctypes.byref(dev)) == 1  # now pinned
+        comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype(dt), comp.reduction.sum)
+        assert_same(b, exp, dt)
+    finally:
+        _lib.check(m.mi_host_unregister(ptr(a)))
+        _lib.check(m.mi_host_unregister(ptr(b)))
+    assert m.mi_pointer_kind(ptr(b), ctypes.byref(dev)) == 2
+    assert t_reg < 30.0

@@ -35,9 +35,9 @@ int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 2000;
     const size_t n = 1024;  // 4 KiB fp32
     float *a, *b, *ha, *hb;
-    hipMalloc(&a, n * 4);
-    hipMalloc(&b, n * 4);
-    hipMemset(a, 0, n * 4);
+    (void)hipMalloc(&a, n * 4);
+    (void)hipMalloc(&b, n * 4);
+    (void)hipMemset(a, 0, n * 4);
     hipMemset(b, 0, n * 4);
     hipHostMalloc(&ha, n * 4, 0);
     hipHostMalloc(&hb, n * 4, 0);
