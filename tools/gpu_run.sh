@@ -65,6 +65,12 @@ for step in "$@"; do
                 > "$GRAFT_REPO_ROOT/$OUT/prof.out" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
             rc=$?; echo "=== prof rc=$rc" | tee -a "$OUT/steps.log"
             [ $rc -eq 0 ] || exit $rc ;;
+        proftrace)
+            (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+                -d "$GRAFT_REPO_ROOT/$OUT/proftrace" -o policy -- "$GRAFT_REPO_ROOT/tools/policy_sweep" 1024 1 3 \
+                > "$GRAFT_REPO_ROOT/$OUT/proftrace.out" 2> "$GRAFT_REPO_ROOT/$OUT/proftrace.err")
+            rc=$?; echo "=== proftrace rc=$rc" | tee -a "$OUT/steps.log"
+            [ $rc -eq 0 ] || exit $rc ;;
         pmc)
             for ctr in FETCH_SIZE WRITE_SIZE; do
                 (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv \
