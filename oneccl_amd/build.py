@@ -6,6 +6,7 @@ oneccl_amd/lib/ and travel with the repo snapshot to the GPU box).
   libccl_comp_hip.so  g++: the drop-in src/comp shim (oneCCL's C++ entry
                       points, include/mi_ccl_comp.h), linked to libmi_reduce.so
   tools/reduce_sweep  hipcc: launch-geometry / load-policy sweep (bench tool)
+  tools/policy_sweep  hipcc: cache-policy / store-form / grid-stride experiment
 """
 from __future__ import annotations
 
@@ -73,6 +74,14 @@ def build_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_policy_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "policy_sweep"
+    src = ROOT / "tools" / "policy_sweep.hip"
+    if src.exists() and (force or _stale(out, [src])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wno-unused-result", "-o", str(out), str(src)])
+    return out
+
+
 def build_latency(force: bool = False) -> Path:
     out = ROOT / "tools" / "latency"
     src = ROOT / "tools" / "latency.hip"
@@ -137,6 +146,7 @@ def build_all(force: bool = False) -> None:
     build_mi_reduce(force)
     build_shim(force)
     build_sweep(force)
+    build_policy_sweep(force)
     build_latency(force)
     build_dropin_caller(force)
     build_asan(force)

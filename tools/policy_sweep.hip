@@ -94,6 +94,51 @@ __global__ __launch_bounds__(B) void w_b64(uint64_t* o, uint32_t tiles) {  // 8-
     for (int j = 0; j < 2 * U; j++) __builtin_nontemporal_store((uint64_t)(base + j), o + base + (size_t)j * B);
 }
 
+// grid-stride streams, the shape of the runtime's fill kernel
+// (__amd_rocclr_fillBufferAligned: one 16-B element per lane per iteration,
+// pointer advanced by the whole grid)
+template <int B, int NT>
+__global__ __launch_bounds__(B) void w_stride(u32x4* o, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * B;
+    for (size_t i = (size_t)blockIdx.x * B + threadIdx.x; i < nvec; i += step) {
+        const u32x4 v{(uint32_t)i, 1u, 2u, 3u};
+        if (NT) __builtin_nontemporal_store(v, o + i);
+        else o[i] = v;
+    }
+}
+
+template <int B, int NT>
+__global__ __launch_bounds__(B) void k_stride(const u32x4* in, u32x4* io, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * B;
+    for (size_t i = (size_t)blockIdx.x * B + threadIdx.x; i < nvec; i += step) {
+        const u32x4 a = __builtin_nontemporal_load(io + i), b = __builtin_nontemporal_load(in + i);
+        const u32x4 x = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, a) + __builtin_bit_cast(f32x4, b));
+        if (NT) __builtin_nontemporal_store(x, io + i);
+        else io[i] = x;
+    }
+}
+
+// persistent sweep with U vectors per lane per iteration: the grid walks one
+// contiguous window of gridDim*B*U vectors at a time (block b owns the b-th
+// B*U slice of the window)
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_window(const u32x4* in, u32x4* io, size_t nvec) {
+    const size_t win = (size_t)gridDim.x * B * U;
+    for (size_t w = (size_t)blockIdx.x * B * U + threadIdx.x; w + (U - 1) * B < nvec; w += win) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) a[j] = __builtin_nontemporal_load(io + w + j * B);
+#pragma unroll
+        for (int j = 0; j < U; j++) b[j] = __builtin_nontemporal_load(in + w + j * B);
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const u32x4 x = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, a[j]) + __builtin_bit_cast(f32x4, b[j]));
+            if (NT) __builtin_nontemporal_store(x, io + w + j * B);
+            else io[w + j * B] = x;
+        }
+    }
+}
+
 struct Variant {
     std::string name;
     std::function<void(hipStream_t)> run;
@@ -103,6 +148,16 @@ struct Variant {
 size_t g_nvec;
 const float* g_in;
 float* g_io;
+
+template <int B, int U, int NT>
+void addwin(std::vector<Variant>& vs, int grid) {
+    char name[128];
+    snprintf(name, sizeof name, "window B=%d U=%d grid=%d st=%s", B, U, grid, NT ? "nt" : "plain");
+    const u32x4* in = (const u32x4*)g_in;
+    u32x4* io = (u32x4*)g_io;
+    const size_t nv = g_nvec;
+    vs.push_back({name, [=](hipStream_t s) { hipLaunchKernelGGL((k_window<B, U, NT>), dim3(grid), dim3(B), 0, s, in, io, nv); }, {}});
+}
 
 template <int B, int U, int LP, int SP, int MAP>
 void addb(std::vector<Variant>& vs) {
@@ -149,11 +204,24 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
 
     std::vector<Variant> vs;
-    addg<256, 4, 1, 0>(vs);  // == the library's configuration
-    addg<1024, 1, 1, 0>(vs);
-    addb<256, 4, 2, 2, 0>(vs);
-    addb<256, 4, 2, 18, 0>(vs);
-
+    addg<256, 4, 1, 0>(vs);
+    addg<1024, 1, 1, 0>(vs);  // == the library's 2-input configuration
+    for (int g : {256, 512}) {
+        addwin<256, 4, 1>(vs, g);
+        addwin<256, 8, 1>(vs, g);
+        addwin<256, 16, 1>(vs, g);
+        addwin<512, 2, 1>(vs, g);
+        addwin<512, 4, 1>(vs, g);
+        addwin<512, 8, 1>(vs, g);
+        addwin<1024, 1, 1>(vs, g);
+        addwin<1024, 2, 1>(vs, g);
+        addwin<1024, 4, 1>(vs, g);
+        addwin<256, 8, 0>(vs, g);
+        addwin<1024, 2, 0>(vs, g);
+    }
+    addwin<256, 4, 1>(vs, 1024);
+    addwin<256, 2, 1>(vs, 1024);
+    addwin<256, 4, 1>(vs, 2048);
     {
         float* wo = io;
         auto addw = [&](const char* name, std::function<void(hipStream_t)> f) {
@@ -168,6 +236,14 @@ int main(int argc, char** argv) {
         addw("buffer B=256 U=4 st=sc1nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 4, 18>), dim3(t4), dim3(256), 0, st, wo, t4); });
         addw("buffer B=256 U=16 st=nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_buffer<256, 16, 2>), dim3(t16), dim3(256), 0, st, wo, t16); });
         addw("b64 B=256 U=4 nt", [=](hipStream_t st) { hipLaunchKernelGGL((w_b64<256, 4>), dim3(t4), dim3(256), 0, st, (uint64_t*)wo, t4); });
+        for (int wg : {128, 256, 512}) {
+            char name[96];
+            const size_t nv = g_nvec;
+            snprintf(name, sizeof name, "stride B=256 grid=%d st=plain", wg);
+            addw(name, [=](hipStream_t st) { hipLaunchKernelGGL((w_stride<256, 0>), dim3(wg), dim3(256), 0, st, (u32x4*)wo, nv); });
+            snprintf(name, sizeof name, "stride B=256 grid=%d st=nt", wg);
+            addw(name, [=](hipStream_t st) { hipLaunchKernelGGL((w_stride<256, 1>), dim3(wg), dim3(256), 0, st, (u32x4*)wo, nv); });
+        }
         addw("hipMemsetAsync", [=](hipStream_t st) { (void)hipMemsetAsync(wo, 0, g_nvec * 16, st); });
     }
     hipEvent_t e0, e1;
