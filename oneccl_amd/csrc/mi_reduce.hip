@@ -133,6 +133,13 @@ typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
 // Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
 constexpr int kB2 = 1024;
 constexpr int kU2 = 1;
+// Buffer-addressed fan-in, one tile per block (profiles/round1_sweep7_fan_buffer*.jsonl).
+// 1024-lane tiles; 256 for 1-byte types, whose unpacked 16 x 16 elements
+// would not fit the 128 VGPRs a 1024-lane block leaves each lane.
+template <typename Tag>
+constexpr int fan_block() {
+    return sizeof(typename Tr<Tag>::S) == 1 ? 256 : 1024;
+}
 
 template <typename Tag, int OP, unsigned V>
 hipError_t launch_general(dim3 grid, hipStream_t s, const KArgs& a) {
@@ -146,11 +153,22 @@ hipError_t launch_lean(dim3 grid, hipStream_t s, const R2Args& a) {
     return hipGetLastError();
 }
 
+template <typename Tag, int OP, unsigned V>
+hipError_t launch_fan(dim3, hipStream_t s, const KArgs& a) {
+    constexpr int B = fan_block<Tag>();
+    const uint64_t blocks = std::max<uint64_t>((a.nvec + B - 1) / B, 1);
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+    hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B>), dim3((unsigned)blocks), dim3(B), 0, s, a);
+    return hipGetLastError();
+}
+
 // general: any K (runtime), grid-stride, also the element loop for operands
-// with different misalignments; lean: K = 2 with a common alignment
+// with different misalignments; lean: K = 2 with a common alignment; fan:
+// any other K with a common alignment
 struct Kern {
     LaunchFn general = nullptr;
     Launch2Fn lean = nullptr;
+    LaunchFn fan = nullptr;
 };
 
 template <typename Tag, int OP, unsigned V>
@@ -170,6 +188,7 @@ Kern entry() {
     if constexpr (valid_v<Tag, OP, V>()) {
         k.general = &launch_general<Tag, OP, V>;
         k.lean = &launch_lean<Tag, OP, V>;
+        k.fan = &launch_fan<Tag, OP, V>;
     }
     return k;
 }
@@ -248,8 +267,11 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
     const uint64_t nvec = same ? (count - head) / n_per_vec : 0;
     const size_t tail = same ? count - head - nvec * n_per_vec : 0;
 
+    // A grid cap (tuning / test knob) routes everything through the
+    // grid-stride general kernel; otherwise one tile per block.
+    const int cap = max_blocks();
     hipError_t e;
-    if (same && k == 2) {
+    if (same && cap == 0 && k == 2) {
         R2Args r;
         r.acc = inputs[0];
         r.in = inputs[1];
@@ -270,22 +292,29 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         a.k = k;
         a.count = count;
         a.trunc_from = trunc_from;
-        uint64_t blocks;
         if (same) {
             a.head = head;
             a.nvec = nvec;
             a.tail = tail;
-            const uint64_t tile = (uint64_t)kBlock * kUnroll;
-            blocks = (a.nvec + tile - 1) / tile;
-            const int cap = max_blocks();
-            if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
-            if (blocks == 0) blocks = 1;
         } else {
             a.scalar_only = 1;
-            blocks = std::min<uint64_t>((count + kBlock - 1) / kBlock, 8192);
         }
-        if (blocks > 0x7FFFFFFFull) blocks = 0x7FFFFFFFull;  // grid-stride covers the rest
-        e = kern.general(dim3((unsigned)blocks), stream, a);
+        // fan tiles are >= 256 vectors: one launch covers 2^39 vectors
+        if (same && cap == 0 && nvec / 256 < 0x7FFFFFFFull) {
+            e = kern.fan(dim3(0), stream, a);
+        } else {
+            uint64_t blocks;
+            if (same) {
+                const uint64_t tile = (uint64_t)kBlock * kUnroll;
+                blocks = (a.nvec + tile - 1) / tile;
+                if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
+                if (blocks == 0) blocks = 1;
+            } else {
+                blocks = std::min<uint64_t>((count + kBlock - 1) / kBlock, 8192);
+            }
+            if (blocks > 0x7FFFFFFFull) blocks = 0x7FFFFFFFull;  // grid-stride covers the rest
+            e = kern.general(dim3((unsigned)blocks), stream, a);
+        }
     }
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;

@@ -474,6 +474,101 @@ __global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Buffer-addressed forms (cdna_hip_programming.md T8/T20).  Each block owns one
+// tile of B vectors.  Every stream gets one SGPR descriptor per tile, built
+// from kernel arguments and blockIdx only (wave-uniform, so no waterfall).
+// Its range is the tile's valid bytes, so in the last tile lanes past the end
+// read zeros and their stores are dropped by the range check: no guard
+// branches.  Lanes carry only a 32-bit byte offset.
+// ---------------------------------------------------------------------------
+constexpr int kAuxNT = 2;  // buffer op aux bit 1: non-temporal (gfx950)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint64_t byte0, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(base) + byte0), (short)0,
+                                             (int)nbytes, 0x00020000);
+}
+
+// Fan-in with a runtime K (2..kMaxInputs): all K loads are issued before the
+// first combine (uniform branches on k only), then the left fold in the
+// reference's order (acc = in[0]; acc = op(in[j], acc)).  Common alignment
+// required; head/tail by block 0 through the scalar element path.
+template <typename Tag, int OP, unsigned V, int B>
+__global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    constexpr int N = 16 / sizeof(S);
+    const int k = a.k;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head) reduce_elem<Tag, OP, V>(a, k, threadIdx.x);
+        if (threadIdx.x < a.tail) reduce_elem<Tag, OP, V>(a, k, a.head + a.nvec * N + threadIdx.x);
+    }
+    const uint64_t t0 = (uint64_t)blockIdx.x * B;
+    if (t0 >= a.nvec) return;
+    const uint64_t left = a.nvec - t0;
+    const uint32_t bytes = (uint32_t)(left < (uint64_t)B ? left : (uint64_t)B) * 16u;
+    const uint64_t byte0 = a.head * sizeof(S) + t0 * 16;
+    const uint32_t off = threadIdx.x * 16u;
+    // Materialise every input pointer before the first branch: left alone, the
+    // compiler sinks each kernarg load into its `i < k` block and every buffer
+    // load then waits on its own scalar load.
+    const void* in[kMaxInputs];
+#pragma unroll
+    for (int i = 0; i < kMaxInputs; i++) {
+        in[i] = a.in[i];
+        asm volatile("" ::"s"(in[i]));
+    }
+    u32x4 x[kMaxInputs];
+#pragma unroll
+    for (int i = 0; i < kMaxInputs; i++)
+        if (i < k) x[i] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], byte0, bytes), off, 0, kAuxNT);
+    C acc[N];
+    const Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0]);
+#pragma unroll
+    for (int e = 0; e < N; e++) acc[e] = widen<Tag>(p0.e[e]);
+#pragma unroll
+    for (int i = 1; i < kMaxInputs; i++) {
+        if (i < k) {
+            const Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i]);
+#pragma unroll
+            for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V>(widen<Tag>(pi.e[e]), acc[e]);
+        }
+    }
+    Pack<S> pr;
+    const uint64_t e0 = a.head + (t0 + threadIdx.x) * N;
+#pragma unroll
+    for (int e = 0; e < N; e++) pr.e[e] = finish<Tag, V>(acc[e], e0 + e, a.trunc_from);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pr), tile_rsrc(a.out, byte0, bytes), off, 0,
+                                           kAuxNT);
+}
+
+// The 2-input form of the same (R2Args: acc, in -> out).
+template <typename Tag, int OP, unsigned V, int B>
+__global__ __launch_bounds__(B) void reduce2b_kernel(R2Args a) {
+    using S = typename Tr<Tag>::S;
+    constexpr int N = 16 / sizeof(S);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head) reduce2_elem<Tag, OP, V>(a, threadIdx.x);
+        if (threadIdx.x < a.tail) reduce2_elem<Tag, OP, V>(a, a.head + a.nvec * N + threadIdx.x);
+    }
+    const uint64_t t0 = (uint64_t)blockIdx.x * B;
+    if (t0 >= a.nvec) return;
+    const uint64_t left = a.nvec - t0;
+    const uint32_t bytes = (uint32_t)(left < (uint64_t)B ? left : (uint64_t)B) * 16u;
+    const uint64_t byte0 = (uint64_t)a.head * sizeof(S) + t0 * 16;
+    const uint32_t off = threadIdx.x * 16u;
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.acc, byte0, bytes), off, 0, kAuxNT);
+    const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in, byte0, bytes), off, 0, kAuxNT);
+    const Pack<S> px = __builtin_bit_cast(Pack<S>, x), py = __builtin_bit_cast(Pack<S>, y);
+    Pack<S> pr;
+    const uint64_t e0 = a.head + (t0 + threadIdx.x) * N;
+#pragma unroll
+    for (int e = 0; e < N; e++)
+        pr.e[e] = finish<Tag, V>(step<Tag, OP, V>(widen<Tag>(py.e[e]), widen<Tag>(px.e[e])), e0 + e, a.trunc_from);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pr), tile_rsrc(a.out, byte0, bytes), off, 0,
+                                           kAuxNT);
+}
+
+// ---------------------------------------------------------------------------
 // element conversions fp32 <-> bf16 / fp16 (ccl_convert_*_arrays,
 // src/comp/bf16/bf16.cpp:113-169, src/comp/fp16/fp16.cpp:55-61)
 // ---------------------------------------------------------------------------

@@ -254,3 +254,73 @@ def test_counts_beyond_32_bit_indices(dt, n):
     _sync()
     got = tb.cpu().numpy().view(st)
     assert_same(got, exp, dt, f"n={n}")
+
+
+# ---- kernel-form coverage ---------------------------------------------------
+
+FAN_OFFS = [(FP32, 0, 5, 3), (BF16, 0, 5, 1), (0, 0, 7, 9), (FP64, 3, 3, 1), (FP16, 1, 4, 5), (6, 2, 16, 1)]
+
+
+@pytest.mark.parametrize("dt,op,k,off", FAN_OFFS, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}-k{k}-off{s}"
+                                                      for d, o, k, s in FAN_OFFS])
+@pytest.mark.parametrize("inplace", [False, True], ids=["out", "inplace"])
+def test_fanin_common_misalignment(dt, op, k, off, inplace):
+    """Fan-in on sub-buffers that share one misalignment (the fan kernel's
+    scalar head + tiled body + partial last tile + scalar tail), written out
+    of place or into input 0 as ccl_comp_batch_reduce does (comp.cpp:236-245)."""
+    n = 3 * 1024 * (16 // oracle.NP_DTYPE[dt]().itemsize) + 29
+    var = VARIANTS[dt][-1]
+    ins = [rand_array(dt, n, seed=300 + 11 * j + dt, op=op) for j in range(k)]
+    exp = oracle.fanin(ins, dt, op, var[2], var[3])
+    holders = [to_dev(x, offset_elems=off) for x in ins]
+    if inplace:
+        to, po = holders[0]
+    else:
+        to, po = to_dev(np.zeros_like(ins[0]), offset_elems=off)
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, k, po, n, dt, op, var[1], _stream()))
+    _sync()
+    assert_same(from_dev(to, ins[0], off), exp, dt)
+
+
+@pytest.mark.parametrize("dt,op,k", [(FP32, 0, 2), (FP32, 3, 6), (BF16, 0, 2), (BF16, 0, 4), (0, 1, 3),
+                                     (FP16, 2, 16), (7, 0, 2)])
+def test_grid_stride_general_kernel(dt, op, k):
+    """A grid cap (mi_set_max_blocks / MI_REDUCE_MAX_BLOCKS) routes every call
+    through the grid-stride general kernel: same results."""
+    m = _lib.mi()
+    n = 200_003
+    var = VARIANTS[dt][-1]
+    ins = [rand_array(dt, n, seed=500 + 13 * j + dt, op=op) for j in range(k)]
+    exp = oracle.fanin(ins, dt, op, var[2], var[3])
+    holders = [to_dev(x) for x in ins]
+    to, po = to_dev(np.zeros_like(ins[0]))
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(m.mi_set_max_blocks(7))
+    try:
+        _lib.check(m.mi_reduce_multi(arr, k, po, n, dt, op, var[1], _stream()))
+        _sync()
+    finally:
+        _lib.check(m.mi_set_max_blocks(0))
+    assert_same(from_dev(to, ins[0]), exp, dt)
+
+
+def test_fanin_beyond_32_bit_indices():
+    """3-input int8 fan-in past 2^32 elements (1-byte types take 256-lane fan
+    tiles: 2^28 blocks)."""
+    import torch
+    n = (1 << 32) + 4099
+    rng = np.random.default_rng(11)
+    ins = [rng.integers(-128, 128, n, dtype=np.int8) for _ in range(3)]
+    exp = ins[0].copy()
+    for x in ins[1:]:
+        oracle.comp_reduce_mt(x, exp, 0, 0, 16)
+    ts = []
+    for j in range(3):
+        ts.append(torch.from_numpy(ins[j]).cuda())
+    del ins
+    arr = _lib.void_ptr_array([t.data_ptr() for t in ts])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, 3, ts[0].data_ptr(), n, 0, 0, 0, _stream()))
+    _sync()
+    got = ts[0].cpu().numpy()
+    assert_same(got, exp, 0, f"n={n}")

@@ -36,7 +36,7 @@ for step in "$@"; do
         smoke)
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         sweep)
-            run sweep 300 ./tools/reduce_sweep 1024 3 10 ;;
+            run sweep 300 ./tools/reduce_sweep 1024 ${SWEEP_ROUNDS:-3} 10 ;;
         policy)
             run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
@@ -58,12 +58,13 @@ for step in "$@"; do
             for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
             done ;;
-        prof)
+        prof)  # PROF_CONFIG=c4 etc. profiles another bench config
+            pc=${PROF_CONFIG:-c2}; pd=prof; [ "$pc" = c2 ] || pd=prof_$pc
             (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-                -d "$GRAFT_REPO_ROOT/$OUT/prof" -o bench -- \
-                python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg \
-                > "$GRAFT_REPO_ROOT/$OUT/prof.out" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
-            rc=$?; echo "=== prof rc=$rc" | tee -a "$OUT/steps.log"
+                -d "$GRAFT_REPO_ROOT/$OUT/$pd" -o bench -- \
+                python3 "$GRAFT_REPO_ROOT/bench.py" --config "$pc" --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg \
+                > "$GRAFT_REPO_ROOT/$OUT/$pd.out" 2> "$GRAFT_REPO_ROOT/$OUT/$pd.err")
+            rc=$?; echo "=== $pd rc=$rc" | tee -a "$OUT/steps.log"
             [ $rc -eq 0 ] || exit $rc ;;
         proftrace)
             (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \

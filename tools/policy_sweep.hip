@@ -139,6 +139,30 @@ __global__ __launch_bounds__(B) void k_window(const u32x4* in, u32x4* io, size_t
     }
 }
 
+// K-input fan-in, in place into input 0 (comp.cpp:217-241 semantics), buffer
+// ops with load/store aux bits LP/SP; LAST0 loads input 0 last (closest to
+// its store)
+template <int K, int B, int LP, int SP, int LAST0>
+__global__ __launch_bounds__(B) void k_fan(const float* const* ins, uint32_t tiles) {
+    const uint32_t t = blockIdx.x;
+    if (t >= tiles) return;
+    const int tb = B * 16;
+    u32x4 x[K];
+#pragma unroll
+    for (int jj = 0; jj < K; jj++) {
+        const int j = LAST0 ? (jj + 1) % K : jj;
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(reinterpret_cast<const char*>(ins[j]) + (size_t)t * tb), (short)0, tb, 0x00020000);
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, threadIdx.x * 16, 0, LP);
+    }
+    f32x4 acc = __builtin_bit_cast(f32x4, x[0]);
+#pragma unroll
+    for (int j = 1; j < K; j++) acc += __builtin_bit_cast(f32x4, x[j]);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(ins[0]) + (size_t)t * tb), (short)0, tb, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), ro, threadIdx.x * 16, 0, SP);
+}
+
 struct Variant {
     std::string name;
     std::function<void(hipStream_t)> run;
@@ -206,22 +230,40 @@ int main(int argc, char** argv) {
     std::vector<Variant> vs;
     addg<256, 4, 1, 0>(vs);
     addg<1024, 1, 1, 0>(vs);  // == the library's 2-input configuration
-    for (int g : {256, 512}) {
+    // fan-in K=8, in place
+    std::vector<float*> fan8(8);
+    fan8[0] = g_io;
+    fan8[1] = const_cast<float*>(g_in);
+    for (int j = 2; j < 8; j++) {
+        CK(hipMalloc(&fan8[j], bytes));
+        CK(hipMemset(fan8[j], 0x3c, bytes));
+    }
+    float** d_fan8 = nullptr;
+    CK(hipMalloc(&d_fan8, 8 * sizeof(float*)));
+    CK(hipMemcpy(d_fan8, fan8.data(), 8 * sizeof(float*), hipMemcpyHostToDevice));
+    {
+        const uint32_t tiles = (uint32_t)(g_nvec / 1024), tiles256 = (uint32_t)(g_nvec / 256);
+        const float* const* dp = d_fan8;
+#define FAN(B, LP, SP, L0, T)                                                                                     \
+    vs.push_back({"FAN8 B=" #B " ld=" #LP " st=" #SP " last0=" #L0, [=](hipStream_t st) {                        \
+                      hipLaunchKernelGGL((k_fan<8, B, LP, SP, L0>), dim3(T), dim3(B), 0, st, dp, T);               \
+                  }, {}})
+        FAN(1024, 2, 2, 0, tiles);
+        FAN(1024, 2, 0, 0, tiles);
+        FAN(1024, 2, 16, 0, tiles);
+        FAN(1024, 2, 18, 0, tiles);
+        FAN(1024, 0, 2, 0, tiles);
+        FAN(1024, 18, 2, 0, tiles);
+        FAN(1024, 2, 2, 1, tiles);
+        FAN(256, 2, 2, 0, tiles256);
+        FAN(256, 2, 0, 0, tiles256);
+        FAN(256, 2, 2, 1, tiles256);
+#undef FAN
+    }
+    for (int g : {256}) {
         addwin<256, 4, 1>(vs, g);
         addwin<256, 8, 1>(vs, g);
-        addwin<256, 16, 1>(vs, g);
-        addwin<512, 2, 1>(vs, g);
-        addwin<512, 4, 1>(vs, g);
-        addwin<512, 8, 1>(vs, g);
-        addwin<1024, 1, 1>(vs, g);
-        addwin<1024, 2, 1>(vs, g);
-        addwin<1024, 4, 1>(vs, g);
-        addwin<256, 8, 0>(vs, g);
-        addwin<1024, 2, 0>(vs, g);
     }
-    addwin<256, 4, 1>(vs, 1024);
-    addwin<256, 2, 1>(vs, 1024);
-    addwin<256, 4, 1>(vs, 2048);
     {
         float* wo = io;
         auto addw = [&](const char* name, std::function<void(hipStream_t)> f) {
@@ -267,7 +309,7 @@ int main(int argc, char** argv) {
         fprintf(stderr, "round %d/%d\n", r + 1, rounds);
     }
     for (auto& v : vs) {
-        const double traffic = (v.name.rfind("WRITE-ONLY", 0) == 0 ? 1.0 : 3.0) * bytes;
+        const double traffic = (v.name.rfind("WRITE-ONLY", 0) == 0 ? 1.0 : v.name.rfind("FAN8", 0) == 0 ? 9.0 : 3.0) * bytes;
         std::sort(v.ms.begin(), v.ms.end());
         const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
         printf("{\"variant\": \"%s\", \"median_ms\": %.5f, \"best_ms\": %.5f, \"median_GBps\": %.1f, "
