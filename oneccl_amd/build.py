@@ -7,6 +7,7 @@ oneccl_amd/lib/ and travel with the repo snapshot to the GPU box).
                       points, include/mi_ccl_comp.h), linked to libmi_reduce.so
   tools/reduce_sweep  hipcc: launch-geometry / load-policy sweep (bench tool)
   tools/policy_sweep  hipcc: cache-policy / store-form / grid-stride experiment
+  tools/fan_sweep     hipcc: fan-in input order experiment
 """
 from __future__ import annotations
 
@@ -82,6 +83,15 @@ def build_policy_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_fan_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "fan_sweep"
+    src = ROOT / "tools" / "fan_sweep.hip"
+    deps = [src, CSRC / "reduce_kernels.hpp"]
+    if src.exists() and (force or _stale(out, deps)):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
 def build_latency(force: bool = False) -> Path:
     out = ROOT / "tools" / "latency"
     src = ROOT / "tools" / "latency.hip"
@@ -147,6 +157,7 @@ def build_all(force: bool = False) -> None:
     build_shim(force)
     build_sweep(force)
     build_policy_sweep(force)
+    build_fan_sweep(force)
     build_latency(force)
     build_dropin_caller(force)
     build_asan(force)

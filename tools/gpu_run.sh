@@ -37,6 +37,10 @@ for step in "$@"; do
             run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         sweep)
             run sweep 300 ./tools/reduce_sweep 1024 ${SWEEP_ROUNDS:-3} 10 ;;
+        fansweep)
+            run fansweep 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
+        fanlayout)
+            run fanlayout 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 layout ;;
         policy)
             run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
