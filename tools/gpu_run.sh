@@ -45,6 +45,10 @@ for step in "$@"; do
             run policy 300 ./tools/policy_sweep 1024 5 10 ;;
         bench)
             run bench 600 python bench.py ;;
+        bench3)  # run-to-run spread of the headline in one box
+            for i in 1 2 3; do run "bench_rep$i" 300 python bench.py --no-cpu-baseline --no-host-leg; done ;;
+        warm)
+            run warm 300 python tools/warm_probe.py ;;
         c1)
             run c1_dropin 300 python tools/c1_allreduce.py --reduce dropin &&
             run c1_oracle 300 python tools/c1_allreduce.py --reduce oracle &&
