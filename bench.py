@@ -238,6 +238,9 @@ def main():
     value = total_bytes * args.steps / elapsed / GiB
     traffic_per_launch = (k + 1) * n * es  # read k inputs, write 1 (algorithmic)
     achieved = traffic_per_launch / (avg_kern_ms / 1e3) / 1e9
+    # whole job: all ranks' launch bytes over the slowest rank's launch time,
+    # against world x one HBM (north star: fraction of aggregate HBM roofline)
+    agg_achieved = (k + 1) * total_bytes / (avg_kern_ms_max / 1e3) / 1e9
 
     # the same bucket through oneCCL's own entry point: ccl_comp_reduce of the
     # drop-in shim (synchronous, as src/sched calls it) — reported beside `value`
@@ -289,6 +292,9 @@ def main():
                          "algorithmic_bytes_per_launch": traffic_per_launch,
                          "avg_kernel_ms": round(avg_kern_ms, 5), "avg_kernel_ms_max_rank": round(avg_kern_ms_max, 5),
                          "kernel_ms_min": round(min(kern_ms), 5),
+                         "aggregate": {"achieved": round(agg_achieved, 1), "peak": HBM_PEAK_GBPS * world,
+                                       "frac": round(agg_achieved / (HBM_PEAK_GBPS * world), 4),
+                                       "note": "all ranks' algorithmic launch bytes / max-over-ranks mean launch time"},
                          "timing": "hipEvent pair around each launch on the launch stream; mean over timed steps",
                          "traffic_source": traffic.get("source") if traffic else None},
             "cpu_baseline": cpu,

@@ -53,6 +53,17 @@ int mi_ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t c
  * src/comp/fp16/fp16.cpp:55-61 */
 int mi_ccl_convert_fp32_to_fp16(const void* src, void* dst);
 int mi_ccl_convert_fp16_to_fp32(const void* src, void* dst);
+/* Asynchronous ccl_comp_reduce (include/mi_ccl_comp_async.hpp, SURVEY.md
+ * §8f rank 4): start issues the reduce and returns a request; test sets
+ * *done = 1 once inout_buf holds the result; free waits if still pending.
+ * `fn` is the user callback for op = custom (run inside start), else NULL. */
+struct ccl_comp_request;
+int mi_ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf,
+                             size_t* out_count, int dtype, int op, mi_ccl_reduction_fn fn,
+                             struct ccl_comp_request** req);
+int mi_ccl_comp_request_test(struct ccl_comp_request* req, int* done);
+int mi_ccl_comp_request_wait(struct ccl_comp_request* req);
+int mi_ccl_comp_request_free(struct ccl_comp_request* req);
 /* ccl_reduction_to_str, src/comp/comp.cpp:251-260 */
 const char* mi_ccl_reduction_to_str(int op);
 /* Re-read CCL_BF16 / CCL_FP16 / CCL_COMP_HIP_DEVICE (env.cpp:711-720). */

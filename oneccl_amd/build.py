@@ -56,7 +56,7 @@ def build_mi_reduce(force: bool = False) -> Path:
 def build_shim(force: bool = False) -> Path:
     out = LIB / "libccl_comp_hip.so"
     deps = [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_reduce.h",
-            ROOT / "include" / "mi_ccl_comp.h", LIB / "libmi_reduce.so"]
+            ROOT / "include" / "mi_ccl_comp.h", ROOT / "include" / "mi_ccl_comp_async.hpp", LIB / "libmi_reduce.so"]
     if force or _stale(out, deps):
         cxx = os.environ.get("CXX", "g++")
         _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
@@ -106,7 +106,7 @@ def build_dropin_caller(force: bool = False) -> Path:
     mangled names (tests/cpp/dropin_caller.cpp)."""
     src = ROOT / "tests" / "cpp" / "dropin_caller.cpp"
     out = ROOT / "tests" / "cpp" / "dropin_caller"
-    deps = [src, CSRC / "ccl_mirror.hpp", LIB / "libccl_comp_hip.so"]
+    deps = [src, CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_ccl_comp_async.hpp", LIB / "libccl_comp_hip.so"]
     if src.exists() and (force or _stale(out, deps)):
         _run([_hipcc(), "-O2", "-std=c++17", "-o", str(out), str(src), f"-L{LIB}", "-lccl_comp_hip",
               "-lmi_reduce", f"-Wl,-rpath,{LIB}", "-Wl,-rpath,$ORIGIN/../../oneccl_amd/lib"])
@@ -126,7 +126,7 @@ def build_asan(force: bool = False) -> Path:
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", *san,
               "-o", str(mi), str(CSRC / "mi_reduce.hip")])
     shim = adir / "libccl_comp_hip.so"
-    if force or _stale(shim, [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", mi]):
+    if force or _stale(shim, [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_ccl_comp_async.hpp", mi]):
         # the same compiler (and so the same ASan runtime) as the hipcc-built pieces
         clang = next((c for c in ("/opt/rocm/lib/llvm/bin/clang++", "/opt/rocm/llvm/bin/clang++")
                       if Path(c).exists()), "clang++")

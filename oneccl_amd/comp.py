@@ -182,6 +182,41 @@ def comp_batch_reduce(in_ptr: int, offsets: Sequence[int], count: int, inout_ptr
     return None if oc.value == 0xFFFFFFFFFFFFFFFF else oc.value
 
 
+class comp_request:
+    """An in-flight ccl_comp_reduce_start (include/mi_ccl_comp_async.hpp).
+    `out_count` is what the reference would have written (bf16/fp16) or None."""
+
+    def __init__(self, handle: int, out_count: Optional[int], keep=None):
+        self._h = handle
+        self.out_count = out_count
+        self._keep = keep  # a ctypes callback must outlive the call
+
+    def test(self) -> bool:
+        done = ctypes.c_int(0)
+        check_shim(shim().mi_ccl_comp_request_test(self._h, ctypes.byref(done)), "ccl_comp_request_test")
+        return bool(done.value)
+
+    def wait(self) -> None:
+        check_shim(shim().mi_ccl_comp_request_wait(self._h), "ccl_comp_request_wait")
+
+    def free(self) -> None:
+        if self._h is not None:
+            h, self._h = self._h, None
+            check_shim(shim().mi_ccl_comp_request_free(h), "ccl_comp_request_free")
+
+
+def comp_reduce_start(in_ptr: int, count: int, inout_ptr: int, dtype: datatype, op: reduction,
+                      fn=None) -> comp_request:
+    """ccl_comp_reduce_start: issue the reduce, return a request to poll
+    (the async form a schedule entry's start()/update() pair would use)."""
+    oc = ctypes.c_size_t(0xFFFFFFFFFFFFFFFF)
+    h = ctypes.c_void_p()
+    cb = _lib.MI_CCL_REDUCTION_FN(fn) if fn is not None else _lib.MI_CCL_REDUCTION_FN()
+    check_shim(shim().mi_ccl_comp_reduce_start(in_ptr, count, inout_ptr, ctypes.byref(oc), int(dtype), int(op), cb,
+                                               ctypes.byref(h)), "ccl_comp_reduce_start")
+    return comp_request(h.value, None if oc.value == 0xFFFFFFFFFFFFFFFF else oc.value, cb)
+
+
 def comp_copy(in_ptr: int, out_ptr: int, nbytes: int, use_nontemporal: bool = False) -> None:
     check_shim(shim().mi_ccl_comp_copy(in_ptr, out_ptr, nbytes, int(use_nontemporal)), "ccl_comp_copy")
 
@@ -208,6 +243,6 @@ def shard_range(count: int, rank: int, world: int, align: int = 256) -> tuple[in
 
 
 __all__ = ["reduction", "datatype", "bf16_impl", "fp16_impl", "reduce", "reduce_out", "reduce_multi",
-           "comp_reduce", "comp_batch_reduce", "comp_copy", "reduction_to_str", "impl_types", "env_reload",
+           "comp_reduce", "comp_reduce_start", "comp_request", "comp_batch_reduce", "comp_copy", "reduction_to_str", "impl_types", "env_reload",
            "shard_range", "bf16_flags", "fp16_flags", "reference_flags", "F_MINMAX_INOUT_FIRST", "F_BF16_RNE",
            "F_ACC_FP32", "F_BF16_TAIL_TRUNC16", "DTYPE_SIZE", "_lib"]

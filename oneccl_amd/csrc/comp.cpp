@@ -22,6 +22,7 @@
 //                      bench (ccl_mirror.hpp; same mangled symbols).
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -35,6 +36,7 @@
 #include "comp/comp.hpp"
 #include "comp/fp16/fp16.hpp"
 #define MI_CCL_THROW(msg) CCL_THROW(msg)
+#include "mi_ccl_comp_async.hpp"  // include/ (on the include path)
 static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
 static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
 static int mi_comp_device() { return -1; }
@@ -42,6 +44,7 @@ static int mi_comp_device() { return -1; }
 #include "../../include/mi_ccl_comp.h"
 #include "ccl_mirror.hpp"
 #define MI_CCL_THROW(msg) throw ccl::exception(msg)
+#include "../../include/mi_ccl_comp_async.hpp"
 #endif
 
 // bf16.cpp:26-30, fp16.cpp:25-39 — referenced by env.cpp:711-720, 1101-1102
@@ -175,6 +178,19 @@ unsigned bf16_flags(ccl_bf16_impl_type impl) {
 bool fp16_flags(ccl_fp16_impl_type impl, unsigned* f) {
     *f = MI_F_MINMAX_INOUT_FIRST;
     return impl == ccl_fp16_f16c || impl == ccl_fp16_avx512f || impl == ccl_fp16_avx512fp16;
+}
+
+// Flags of a 2-input reduce of `dt` under the impl types in force (the
+// semantic selection of comp.cpp:96-114 -> bf16.cpp / fp16.cpp).  false: the
+// reference computes nothing (fp16 impl outside f16c/avx512f/avx512fp16).
+bool reduce_semantics(int dt, unsigned* f) {
+    *f = 0u;  // CCL_REDUCE: std::min/std::max operand order
+    if (dt == MI_BFLOAT16) {
+        *f = bf16_flags(mi_bf16_impl());
+        return true;
+    }
+    if (dt == MI_FLOAT16) return fp16_flags(mi_fp16_impl(), f);
+    return true;
 }
 
 void check(int rc, const char* where) {
@@ -374,6 +390,65 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
 
 const char* ccl_reduction_to_str(ccl::reduction type) { return mi_reduction_to_str(static_cast<int>(type)); }
 
+// ---- asynchronous ccl_comp_reduce (include/mi_ccl_comp_async.hpp) --------
+struct ccl_comp_request {
+    mi_request_t r = nullptr;  // null: completed inside start (empty, custom, fp16 no-op)
+};
+
+ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
+                                  const ccl_datatype& dtype, ccl::reduction reduction, ccl::reduction_fn reduction_fn,
+                                  const ccl::fn_context* context, ccl_comp_request** req) {
+    if (!req) MI_CCL_THROW("null request pointer");
+    *req = nullptr;
+    std::unique_ptr<ccl_comp_request> q(new ccl_comp_request());
+    if (in_count) {  // comp.cpp:132-134
+        if (reduction == ccl::reduction::custom) {
+            run_custom(in_buf, in_count, inout_buf, out_count, dtype, reduction_fn, context);
+        } else {
+            const int dt = dtype_id(dtype);
+            if (mi_dtype_size(dt) == 0) MI_CCL_THROW("unexpected value " + std::to_string(dt));
+            if ((dt == MI_BFLOAT16 || dt == MI_FLOAT16) && out_count) *out_count = in_count;
+            unsigned f = 0;
+            if (reduce_semantics(dt, &f)) {
+                const void* ins[2] = {inout_buf, in_buf};
+                check(mi_reduce_start(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f,
+                                      mi_comp_device(), &q->r),
+                      "mi_reduce_start");
+            }
+        }
+    }
+    *req = q.release();
+    return ccl::status::success;
+}
+
+bool ccl_comp_request_test(ccl_comp_request* req) {
+    if (!req) MI_CCL_THROW("null request");
+    if (!req->r) return true;
+    int done = 0;
+    check(mi_test(req->r, &done), "mi_test");
+    return done != 0;
+}
+
+void ccl_comp_request_wait(ccl_comp_request* req) {
+    if (!req) MI_CCL_THROW("null request");
+    if (req->r) check(mi_wait(req->r), "mi_wait");
+}
+
+// Waits first if the request is still pending: freeing must never leave a
+// kernel writing into a buffer its owner already considers free.
+void ccl_comp_request_free(ccl_comp_request* req) {
+    if (!req) return;
+    if (req->r) {
+        const int rc = mi_wait(req->r);
+        (void)mi_request_free(req->r);
+        req->r = nullptr;
+        delete req;
+        check(rc, "mi_wait");
+        return;
+    }
+    delete req;
+}
+
 #ifndef MI_ONECCL_TREE
 // ===========================================================================
 // C view of the shim (include/mi_ccl_comp.h) — lets tests and ctypes/FFI
@@ -458,6 +533,35 @@ int mi_ccl_convert_fp32_to_fp16(const void* src, void* dst) {
 int mi_ccl_convert_fp16_to_fp32(const void* src, void* dst) {
     MI_SHIM_GUARD({
         ccl_convert_fp16_to_fp32(src, dst);
+        return 0;
+    });
+}
+
+int mi_ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype,
+                             int op, mi_ccl_reduction_fn fn, struct ccl_comp_request** req) {
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce_start(in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                                    static_cast<ccl::reduction>(op),
+                                                    reinterpret_cast<ccl::reduction_fn>(fn), nullptr, req));
+}
+
+int mi_ccl_comp_request_test(struct ccl_comp_request* req, int* done) {
+    MI_SHIM_GUARD({
+        if (!done) throw ccl::exception("null done pointer");
+        *done = ccl_comp_request_test(req) ? 1 : 0;
+        return 0;
+    });
+}
+
+int mi_ccl_comp_request_wait(struct ccl_comp_request* req) {
+    MI_SHIM_GUARD({
+        ccl_comp_request_wait(req);
+        return 0;
+    });
+}
+
+int mi_ccl_comp_request_free(struct ccl_comp_request* req) {
+    MI_SHIM_GUARD({
+        ccl_comp_request_free(req);
         return 0;
     });
 }

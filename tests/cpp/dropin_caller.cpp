@@ -14,6 +14,34 @@
 #include <vector>
 
 #include "../../oneccl_amd/csrc/ccl_mirror.hpp"
+#include "../../include/mi_ccl_comp_async.hpp"
+
+// reduce_local_entry as INTEGRATION.md §2(d) patches it: start() issues the
+// reduce and returns `started`; the worker's progress loop calls update()
+// until the entry is complete (src/sched/entry/reduce_local_entry.cpp:116-131,
+// src/exec/thread/worker.cpp:310-379).
+enum entry_status { not_started, started, complete };
+struct async_reduce_entry {
+    const void* in;
+    void* inout;
+    size_t cnt;
+    ccl_datatype dtype;
+    ccl::reduction op;
+    entry_status status = not_started;
+    ccl_comp_request* req = nullptr;
+    void start() {
+        ccl_comp_reduce_start(in, cnt, inout, nullptr, dtype, op, nullptr, nullptr, &req);
+        status = started;
+        update();
+    }
+    void update() {
+        if (status == started && ccl_comp_request_test(req)) {
+            ccl_comp_request_free(req);
+            req = nullptr;
+            status = complete;
+        }
+    }
+};
 
 static int failures = 0;
 #define EXPECT(cond, ...)                         \
@@ -165,6 +193,66 @@ int main() {
         bool okk = true;
         for (size_t i = 0; i < f.size(); i++) okk = okk && std::fabs(back[i] - f[i]) <= f[i] / 64;
         EXPECT(okk, "bf16 arrays round trip");
+    }
+
+    // asynchronous entries: 4 device + 2 host-staging reduces in flight, one
+    // progress loop polling them (bounded: a lost completion fails the test)
+    {
+        const size_t m = 1u << 20;
+        const int nd = 4, nh = 2;
+        std::vector<float*> dbufs;
+        std::vector<float> hv(m);
+        for (int e = 0; e < 2 * nd; e++) {
+            float* p = nullptr;
+            if (hipMalloc(&p, m * 4) != hipSuccess) {
+                fprintf(stderr, "hipMalloc failed\n");
+                return 2;
+            }
+            for (size_t i = 0; i < m; i++) hv[i] = (float)((i + (size_t)e) % 251);
+            (void)hipMemcpy(p, hv.data(), m * 4, hipMemcpyHostToDevice);
+            dbufs.push_back(p);
+        }
+        std::vector<float*> hbufs;
+        for (int e = 0; e < 2 * nh; e++) {
+            float* p = static_cast<float*>(staging_alloc(m * 4));
+            for (size_t i = 0; i < m; i++) p[i] = (float)((i + (size_t)e) % 251);
+            hbufs.push_back(p);
+        }
+        std::vector<async_reduce_entry> entries;
+        for (int e = 0; e < nd; e++)
+            entries.push_back({dbufs[2 * e], dbufs[2 * e + 1], m, f32, ccl::reduction::sum});
+        for (int e = 0; e < nh; e++)
+            entries.push_back({hbufs[2 * e], hbufs[2 * e + 1], m, f32, ccl::reduction::max});
+        for (auto& en : entries) en.start();
+        size_t spins = 0;
+        bool all = false;
+        while (!all && spins < 200000000) {
+            all = true;
+            for (auto& en : entries) {
+                en.update();
+                all = all && en.status == complete;
+            }
+            spins++;
+        }
+        EXPECT(all, "async entries did not complete");
+        bool okk = true;
+        for (int e = 0; e < nd; e++) {
+            (void)hipMemcpy(hv.data(), dbufs[2 * e + 1], m * 4, hipMemcpyDeviceToHost);
+            for (size_t i = 0; i < m; i++)
+                okk = okk && hv[i] == (float)((i + 2 * e) % 251) + (float)((i + 2 * e + 1) % 251);
+        }
+        EXPECT(okk, "async device sum");
+        okk = true;
+        for (int e = 0; e < nh; e++)
+            for (size_t i = 0; i < m; i++)
+                okk = okk && hbufs[2 * e + 1][i] == std::fmax((float)((i + 2 * e) % 251), (float)((i + 2 * e + 1) % 251));
+        EXPECT(okk, "async host max");
+        // empty reduce: complete at start (comp.cpp:132-134)
+        async_reduce_entry z{hbufs[0], hbufs[1], 0, f32, ccl::reduction::sum};
+        z.start();
+        EXPECT(z.status == complete, "empty async reduce completes at start");
+        for (float* p : dbufs) (void)hipFree(p);
+        for (float* p : hbufs) free(p);
     }
 
     free(comm_buf);

@@ -61,6 +61,32 @@ def test_shim_exports_onecll_mangled_entry_points():
         assert w in out, w
 
 
+def test_shim_exports_async_entry_points():
+    """The asynchronous form declared in include/mi_ccl_comp_async.hpp."""
+    out = subprocess.run(["nm", "-DC", "--defined-only", str(ROOT / "oneccl_amd/lib/libccl_comp_hip.so")],
+                         check=True, capture_output=True, text=True).stdout
+    for w in ["ccl_comp_reduce_start(void const*, unsigned long, void*, unsigned long*, ccl_datatype const&, "
+              "ccl::v1::reduction, void (*)(void const*, unsigned long, void*, unsigned long*, ccl::v1::datatype, "
+              "ccl::v1::fn_context const*), ccl::v1::fn_context const*, ccl_comp_request**)",
+              "ccl_comp_request_test(ccl_comp_request*)", "ccl_comp_request_wait(ccl_comp_request*)",
+              "ccl_comp_request_free(ccl_comp_request*)"]:
+        assert w in out, w
+
+
+def test_async_empty_reduce_needs_no_device():
+    """in_count == 0 completes inside start without touching HIP
+    (comp.cpp:132-134); a null request pointer is an error."""
+    from oneccl_amd import comp
+    buf = (ctypes.c_float * 4)(1, 2, 3, 4)
+    req = comp.comp_reduce_start(ctypes.addressof(buf), 0, ctypes.addressof(buf), comp.datatype.float32,
+                                 comp.reduction.sum)
+    assert req.test()
+    req.free()
+    assert list(buf) == [1, 2, 3, 4]
+    rc = _lib.shim().mi_ccl_comp_reduce_start(None, 1, None, None, 9, 0, _lib.MI_CCL_REDUCTION_FN(), None)
+    assert rc == -1 and b"null request" in _lib.shim().mi_ccl_last_error()
+
+
 def test_reduction_to_str_matches_reference():
     # src/comp/comp.cpp:251-260
     m = _lib.mi()

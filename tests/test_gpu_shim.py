@@ -353,3 +353,120 @@ def test_registered_staging_buffer_takes_zero_copy(dt):
         _lib.check(m.mi_host_unregister(ptr(b)))
     assert m.mi_pointer_kind(ptr(b), ctypes.byref(dev)) == 2
     assert t_reg < 30.0
+
+
+# ---- asynchronous ccl_comp_reduce (include/mi_ccl_comp_async.hpp, §8f rank 4)
+
+def _poll(req, limit_s=60.0):
+    """A worker's progress loop: poll update() until the entry completes."""
+    import time
+    t0 = time.perf_counter()
+    while not req.test():
+        assert time.perf_counter() - t0 < limit_s, "async reduce did not complete"
+
+
+@pytest.mark.parametrize("where", ["device", "pinned", "pageable"])
+@pytest.mark.parametrize("dt", [FP32, BF16, FP16, 6])
+@pytest.mark.parametrize("op", OPS, ids=[OP_NAME[o] for o in OPS])
+def test_comp_reduce_start_matches_sync(where, dt, op):
+    """start + test polling gives the bits and out_count of ccl_comp_reduce."""
+    import torch
+    n = 70_001
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=31 + op, op=op)
+    b = rand_array(dt, n, seed=41 + op, op=op)
+    exp = b.copy()
+    oc_ref = oracle.comp_reduce(a, exp, dt, op, b_impl, f_impl)
+    keep = []
+    if where == "device":
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        keep += [ta, tb]
+    elif where == "pinned":
+        ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        pa, pb = ha.data_ptr(), hb.data_ptr()
+    else:
+        hb = b.copy()
+        pa, pb = ptr(a), ptr(hb)
+    req = comp.comp_reduce_start(pa, n, pb, comp.datatype(dt), comp.reduction(op))
+    try:
+        _poll(req)
+    finally:
+        req.free()
+    if where == "device":
+        got = from_dev(tb, b)
+    elif where == "pinned":
+        got = hb.numpy().view(b.dtype)
+    else:
+        got = hb
+    assert_same(got, exp, dt, where)
+    assert req.out_count == oc_ref
+
+
+def test_comp_reduce_start_many_in_flight():
+    """Eight entries started before any is polled (one worker's queue), each
+    on its own device buffers; all complete with the right bits."""
+    n = (4 << 20) + 5
+    jobs = []
+    for e in range(8):
+        dt = [FP32, BF16, 4, 6][e % 4]
+        a = rand_array(dt, n, seed=200 + e, specials=False)
+        b = rand_array(dt, n, seed=300 + e, specials=False)
+        exp = b.copy()
+        b_impl, f_impl = impls()
+        oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        jobs.append((dt, b, exp, ta, tb, comp.comp_reduce_start(pa, n, pb, comp.datatype(dt), comp.reduction.sum)))
+    pending = [j[-1] for j in jobs]
+    import time
+    t0 = time.perf_counter()
+    while pending:
+        pending = [r for r in pending if not r.test()]
+        assert time.perf_counter() - t0 < 60
+    for dt, b, exp, ta, tb, req in jobs:
+        req.free()
+        assert_same(from_dev(tb, b), exp, dt)
+
+
+def test_comp_reduce_start_custom_and_empty_complete_at_start():
+    """Custom ops run the user callback inside start (host code, comp.cpp:84-88);
+    in_count == 0 does nothing (comp.cpp:132-134): both requests are complete
+    on return."""
+    n = 1000
+    a = np.arange(n, dtype=np.float32)
+    b = np.ones(n, dtype=np.float32)
+    calls = []
+
+    def fn(in_p, count, inout_p, out_count, dtype, ctx):
+        calls.append(count)
+        src = np.ctypeslib.as_array(ctypes.cast(in_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst = np.ctypeslib.as_array(ctypes.cast(inout_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst += 2 * src
+
+    req = comp.comp_reduce_start(ptr(a), n, ptr(b), comp.datatype.float32, comp.reduction.custom, fn=fn)
+    assert req.test()
+    req.free()
+    assert calls == [n] and np.array_equal(b, 1 + 2 * a)
+    b2 = np.full(n, 7, np.float32)
+    req = comp.comp_reduce_start(ptr(a), 0, ptr(b2), comp.datatype.float32, comp.reduction.sum)
+    assert req.test()
+    req.wait()
+    req.free()
+    assert (b2 == 7).all()
+    with pytest.raises(_lib.MiReduceError):  # custom without a callback (comp.cpp:85)
+        comp.comp_reduce_start(ptr(a), n, ptr(b), comp.datatype.float32, comp.reduction.custom)
+
+
+def test_comp_request_free_waits_for_pending():
+    """Freeing a request still in flight waits for it, so the buffer is never
+    written after its owner reclaims it."""
+    n = (256 << 20) // 4
+    import torch
+    x = torch.full((n,), 1.5, device="cuda")
+    y = torch.full((n,), 2.0, device="cuda")
+    torch.cuda.synchronize()
+    req = comp.comp_reduce_start(x.data_ptr(), n, y.data_ptr(), comp.datatype.float32, comp.reduction.sum)
+    req.free()
+    assert bool((y == 3.5).all())
