@@ -133,12 +133,12 @@ typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
 // Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
 constexpr int kB2 = 1024;
 constexpr int kU2 = 1;
-// Buffer-addressed fan-in, one tile per block (profiles/round1_sweep7_fan_buffer*.jsonl).
-// 1024-lane tiles; 256 for 1-byte types, whose unpacked 16 x 16 elements
-// would not fit the 128 VGPRs a 1024-lane block leaves each lane.
+// Buffer-addressed fan-in, one tile per block (profiles/round1_sweep7_fan_buffer*.jsonl),
+// 1024-lane tiles for every type: 8- and 16-bit integers fold packed on dwords
+// (pk_op4), so no type unpacks more than 8 elements per vector.
 template <typename Tag>
 constexpr int fan_block() {
-    return sizeof(typename Tr<Tag>::S) == 1 ? 256 : 1024;
+    return 1024;
 }
 
 template <typename Tag, int OP, unsigned V>

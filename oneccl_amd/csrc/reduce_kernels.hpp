@@ -217,6 +217,92 @@ struct alignas(16) Pack {
     S e[16 / sizeof(S)];
 };
 
+// ---------------------------------------------------------------------------
+// Packed 8- and 16-bit integer ops on whole dwords: acc' = op(in, acc) per
+// byte / half, with CCL_REDUCE's wrap-around sum and prod.  Unpacking 16 bytes
+// of each of up to 16 inputs cost the fan-in 258 VGPRs, one wave per SIMD and
+// 1.7 TB/s (profiles/round1_misalign.jsonl).  Packed, the fold stays in the 4
+// dwords of the loaded vector.  16-bit lanes map to gfx950's v_pk_*_{i,u}16;
+// bytes run as even/odd halves of those, and sum uses the carry-free SWAR add.
+// min/max of integers have no tie or NaN cases, so operand order is moot.
+// ---------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+template <typename V2>
+__device__ __forceinline__ V2 as2(uint32_t x) { return __builtin_bit_cast(V2, x); }
+template <typename V2>
+__device__ __forceinline__ uint32_t as1(V2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+template <int OP, bool SIGNED>
+__device__ __forceinline__ uint32_t pk16_op(uint32_t in, uint32_t acc) {
+    if constexpr (OP == OP_SUM) return as1(as2<u16x2>(acc) + as2<u16x2>(in));
+    if constexpr (OP == OP_PROD) return as1(as2<u16x2>(acc) * as2<u16x2>(in));
+    if constexpr (SIGNED) {
+        if constexpr (OP == OP_MIN) return as1(__builtin_elementwise_min(as2<i16x2>(acc), as2<i16x2>(in)));
+        if constexpr (OP == OP_MAX) return as1(__builtin_elementwise_max(as2<i16x2>(acc), as2<i16x2>(in)));
+    } else {
+        if constexpr (OP == OP_MIN) return as1(__builtin_elementwise_min(as2<u16x2>(acc), as2<u16x2>(in)));
+        if constexpr (OP == OP_MAX) return as1(__builtin_elementwise_max(as2<u16x2>(acc), as2<u16x2>(in)));
+    }
+}
+
+template <int OP, bool SIGNED>
+__device__ __forceinline__ uint32_t pk8_op(uint32_t in, uint32_t acc) {
+    constexpr uint32_t lo7 = 0x7F7F7F7Fu, hi1 = 0x80808080u, evn = 0x00FF00FFu;
+    if constexpr (OP == OP_SUM) return ((acc & lo7) + (in & lo7)) ^ ((acc ^ in) & hi1);
+    if constexpr (OP == OP_PROD) {  // low byte of each 16-bit product
+        const uint32_t pe = as1(as2<u16x2>(acc & evn) * as2<u16x2>(in & evn));
+        const uint32_t po = as1(as2<u16x2>((acc >> 8) & evn) * as2<u16x2>((in >> 8) & evn));
+        return (pe & evn) | ((po & evn) << 8);
+    }
+    if constexpr (SIGNED) {  // sign-extend even / odd bytes into 16-bit lanes
+        const i16x2 ae = as2<i16x2>(acc << 8) >> 8, ie = as2<i16x2>(in << 8) >> 8;
+        const i16x2 ao = as2<i16x2>(acc) >> 8, io = as2<i16x2>(in) >> 8;
+        i16x2 re, ro;
+        if constexpr (OP == OP_MIN) {
+            re = __builtin_elementwise_min(ae, ie);
+            ro = __builtin_elementwise_min(ao, io);
+        } else {
+            re = __builtin_elementwise_max(ae, ie);
+            ro = __builtin_elementwise_max(ao, io);
+        }
+        return (as1(re) & evn) | ((as1(ro) & evn) << 8);
+    } else {
+        const u16x2 ae = as2<u16x2>(acc & evn), ie = as2<u16x2>(in & evn);
+        const u16x2 ao = as2<u16x2>((acc >> 8) & evn), io = as2<u16x2>((in >> 8) & evn);
+        u16x2 re, ro;
+        if constexpr (OP == OP_MIN) {
+            re = __builtin_elementwise_min(ae, ie);
+            ro = __builtin_elementwise_min(ao, io);
+        } else {
+            re = __builtin_elementwise_max(ae, ie);
+            ro = __builtin_elementwise_max(ao, io);
+        }
+        return as1(re) | (as1(ro) << 8);
+    }
+}
+
+// 8/16-bit integer storage: the fold runs packed on dwords
+template <typename Tag>
+constexpr bool packed_int() {
+    return std::is_integral<Tag>::value && sizeof(Tag) <= 2;
+}
+
+template <typename Tag, int OP>
+__device__ __forceinline__ u32x4 pk_op4(u32x4 in, u32x4 acc) {
+    constexpr bool sg = std::is_signed<Tag>::value;
+    u32x4 r;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        if constexpr (sizeof(Tag) == 1)
+            r[d] = pk8_op<OP, sg>(in[d], acc[d]);
+        else
+            r[d] = pk16_op<OP, sg>(in[d], acc[d]);
+    }
+    return r;
+}
+
 // scalar path for one element (head/tail/misaligned)
 template <typename Tag, int OP, unsigned V>
 __device__ __forceinline__ void reduce_elem(const KArgs& a, int k, uint64_t idx) {
@@ -521,6 +607,14 @@ __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
 #pragma unroll
     for (int i = 0; i < kMaxInputs; i++)
         if (i < k) x[i] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], byte0, bytes), off, 0, kAuxNT);
+    if constexpr (packed_int<Tag>()) {
+        u32x4 r = x[0];
+#pragma unroll
+        for (int i = 1; i < kMaxInputs; i++)
+            if (i < k) r = pk_op4<Tag, OP>(x[i], r);
+        __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
+        return;
+    }
     C acc[N];
     const Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0]);
 #pragma unroll

@@ -256,6 +256,25 @@ def test_counts_beyond_32_bit_indices(dt, n):
     assert_same(got, exp, dt, f"n={n}")
 
 
+PACKED = [(dt, op, k) for dt in (0, 1, 2, 3) for op in OPS for k in (3, 8, 16)]
+
+
+@pytest.mark.parametrize("dt,op,k", PACKED, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}-k{k}" for d, o, k in PACKED])
+def test_fanin_packed_small_ints(dt, op, k):
+    """8- and 16-bit integer fan-in folds packed on dwords (pk_op4): every
+    op, signed and unsigned extremes, wrap-around sum and prod, a partial
+    last tile and a scalar tail."""
+    n = 3 * 16384 + 16 * 5 + 7
+    ins = [rand_array(dt, n, seed=700 + 31 * j + dt, op=op) for j in range(k)]
+    exp = oracle.fanin(ins, dt, op)
+    holders = [to_dev(x) for x in ins]
+    to, po = to_dev(np.zeros_like(ins[0]))
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, k, po, n, dt, op, 0, _stream()))
+    _sync()
+    assert_same(from_dev(to, ins[0]), exp, dt)
+
+
 # ---- kernel-form coverage ---------------------------------------------------
 
 FAN_OFFS = [(FP32, 0, 5, 3), (BF16, 0, 5, 1), (0, 0, 7, 9), (FP64, 3, 3, 1), (FP16, 1, 4, 5), (6, 2, 16, 1)]
