@@ -226,6 +226,13 @@ int mi_set_host_mode(int mode);
 #define MI_SYNC_BLOCK 1
 int mi_set_sync_mode(int mode);
 
+/* Operands whose addresses differ mod 16 bytes (ring chunks at arbitrary
+ * element offsets): 1 (default) = the 16-byte vector kernels on the output's
+ * 16-byte grid, inputs read by unaligned 16-byte loads; 0 = the element loop.
+ * Same bits either way.  Env MI_REDUCE_UNALIGNED=0|1.  Returns the previous
+ * setting.                                                                 */
+int mi_set_unaligned_vectors(int on);
+
 /* ---- introspection ---------------------------------------------------- */
 
 /* ccl_reduction_to_str, src/comp/comp.cpp:251-260. */

@@ -61,6 +61,7 @@ MI_API = [
     ("mi_set_max_blocks", c_int, [c_int]),
     ("mi_set_host_mode", c_int, [c_int]),
     ("mi_set_sync_mode", c_int, [c_int]),
+    ("mi_set_unaligned_vectors", c_int, [c_int]),
 ]
 
 # mirrors include/mi_ccl_comp.h

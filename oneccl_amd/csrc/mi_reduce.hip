@@ -83,6 +83,20 @@ int host_mode() {
     return v;
 }
 
+// Operands whose misalignments differ take the vector kernels (1, default)
+// or the element loop (0).  Env MI_REDUCE_UNALIGNED=0 selects the loop.
+std::atomic<int> g_unaligned{-1};  // -1 = not yet read from env
+
+int unaligned_vectors() {
+    int v = g_unaligned.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* s = getenv("MI_REDUCE_UNALIGNED");
+        v = (s && strcmp(s, "0") == 0) ? 0 : 1;
+        g_unaligned.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
 int max_blocks() {
     int v = g_max_blocks.load(std::memory_order_relaxed);
     if (v < 0) {
@@ -257,21 +271,33 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
     // VCVTNEPS2BF16 main part / scalar tail split of ccl_convert_fp32_to_bf16_arrays
     const uint64_t trunc_from = (count / 16) * 16;
 
-    // common misalignment -> scalar head + vector body + scalar tail;
-    // different misalignments -> element loop (general kernel)
+    // The vector grid is the output's 16-byte grid: a scalar head up to the
+    // first 16-byte boundary of `out`, a vector body, a scalar tail.  Inputs
+    // need only be aligned to their element size: gfx950 serves a 16-byte
+    // load from any byte address (profiles/round1_unaligned_probe.jsonl: right
+    // bytes at every offset; 98-99 % of the aligned stream rate at 4-byte
+    // offsets, 89 % at 1- and 2-byte offsets), so ring chunks at arbitrary
+    // element offsets still stream as 16-byte vectors.  Operands that are not
+    // aligned to their element size take the element loop (general kernel).
     const uintptr_t mis = reinterpret_cast<uintptr_t>(out) & 15u;
-    bool same = (mis % es) == 0;
-    for (int i = 0; i < k && same; i++) same = ((reinterpret_cast<uintptr_t>(inputs[i]) & 15u) == mis);
+    bool elem = (mis % es) == 0;
+    bool same = elem;
+    for (int i = 0; i < k; i++) {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(inputs[i]);
+        elem = elem && (p % es) == 0;
+        same = same && (p & 15u) == mis;
+    }
+    const bool vec = same || (elem && unaligned_vectors());
     const size_t n_per_vec = 16 / es;
-    const size_t head = same && mis ? std::min<size_t>((16 - mis) / es, count) : 0;
-    const uint64_t nvec = same ? (count - head) / n_per_vec : 0;
-    const size_t tail = same ? count - head - nvec * n_per_vec : 0;
+    const size_t head = vec && mis ? std::min<size_t>((16 - mis) / es, count) : 0;
+    const uint64_t nvec = vec ? (count - head) / n_per_vec : 0;
+    const size_t tail = vec ? count - head - nvec * n_per_vec : 0;
 
     // A grid cap (tuning / test knob) routes everything through the
     // grid-stride general kernel; otherwise one tile per block.
     const int cap = max_blocks();
     hipError_t e;
-    if (same && cap == 0 && k == 2) {
+    if (vec && cap == 0 && k == 2) {
         R2Args r;
         r.acc = inputs[0];
         r.in = inputs[1];
@@ -292,7 +318,7 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         a.k = k;
         a.count = count;
         a.trunc_from = trunc_from;
-        if (same) {
+        if (vec) {
             a.head = head;
             a.nvec = nvec;
             a.tail = tail;
@@ -300,11 +326,11 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
             a.scalar_only = 1;
         }
         // fan tiles are >= 256 vectors: one launch covers 2^39 vectors
-        if (same && cap == 0 && nvec / 256 < 0x7FFFFFFFull) {
+        if (vec && cap == 0 && nvec / 256 < 0x7FFFFFFFull) {
             e = kern.fan(dim3(0), stream, a);
         } else {
             uint64_t blocks;
-            if (same) {
+            if (vec) {
                 const uint64_t tile = (uint64_t)kBlock * kUnroll;
                 blocks = (a.nvec + tile - 1) / tile;
                 if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
@@ -904,6 +930,12 @@ int mi_set_sync_mode(int mode) {
     if (mode != MI_SYNC_SPIN && mode != MI_SYNC_BLOCK) return fail(MI_E_INVALID, "bad sync mode");
     const int prev = sync_mode();
     g_sync_mode.store(mode, std::memory_order_relaxed);
+    return prev;
+}
+
+int mi_set_unaligned_vectors(int on) {
+    const int prev = unaligned_vectors();
+    g_unaligned.store(on ? 1 : 0, std::memory_order_relaxed);
     return prev;
 }
 

@@ -77,6 +77,62 @@ def test_misaligned_pointers(dt, off_in, off_io):
     assert_same(got, exp, dt, f"offsets {off_in},{off_io}")
 
 
+UNALIGNED = [(dt, op) for dt in ALL_DTYPES for op in OPS]
+
+
+@pytest.fixture
+def unaligned_mode():
+    """Restore the library's handling of differing misalignments after a test."""
+    m = _lib.mi()
+    prev = m.mi_set_unaligned_vectors(1)
+    yield m
+    m.mi_set_unaligned_vectors(prev)
+
+
+@pytest.mark.parametrize("dt,op", UNALIGNED, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}" for d, o in UNALIGNED])
+@pytest.mark.parametrize("vectors", [1, 0], ids=["unaligned-vectors", "element-loop"])
+def test_differing_misalignment_2input(dt, op, vectors, unaligned_mode):
+    """Ring chunks whose addresses differ mod 16 (element offsets that are not
+    multiples of 16 / size): the vector kernels reading unaligned 16-byte
+    vectors, and the element loop, both bit-exact to the oracle.  Several
+    tiles, partial last tile, scalar head and tail."""
+    es = oracle.NP_DTYPE[dt]().itemsize
+    n = 3 * 16384 + 16 * 7 + 5
+    var = VARIANTS[dt][-1]
+    a = rand_array(dt, n, seed=900 + dt + 13 * op, op=op)
+    b = rand_array(dt, n, seed=950 + dt + 13 * op, op=op)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, op, var[2], var[3])
+    unaligned_mode.mi_set_unaligned_vectors(vectors)
+    off_in, off_io = (1, 0) if es >= 8 else (16 // es - 1, 1)  # differ mod 16 bytes
+    got = gpu_reduce(a, b, dt, op, var[1], off_in, off_io)
+    assert_same(got, exp, dt, f"offsets {off_in},{off_io}")
+
+
+FAN_UNALIGNED = [(FP32, 0, 5), (BF16, 0, 8), (0, 3, 4), (FP16, 2, 3), (FP64, 1, 6), (3, 0, 16), (6, 0, 9)]
+
+
+@pytest.mark.parametrize("dt,op,k", FAN_UNALIGNED, ids=[f"{DT_NAME[d]}-{OP_NAME[o]}-k{k}" for d, o, k in FAN_UNALIGNED])
+@pytest.mark.parametrize("inplace", [False, True], ids=["out", "inplace"])
+def test_differing_misalignment_fanin(dt, op, k, inplace, unaligned_mode):
+    """K-input fan-in with a different element offset per input (and for the
+    output), through the buffer-addressed fan kernel on unaligned bases."""
+    n = 2 * 16384 + 16 * 3 + 9
+    var = VARIANTS[dt][-1]
+    ins = [rand_array(dt, n, seed=1200 + 31 * j + dt, op=op) for j in range(k)]
+    exp = oracle.fanin(ins, dt, op, var[2], var[3])
+    holders = [to_dev(x, pad_elems=16, offset_elems=(j * 3 + 1) % 7) for j, x in enumerate(ins)]
+    if inplace:
+        to, po, off_o = holders[0][0], holders[0][1], 1
+    else:
+        off_o = 2
+        to, po = to_dev(np.zeros_like(ins[0]), pad_elems=16, offset_elems=off_o)
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, k, po, n, dt, op, var[1], _stream()))
+    _sync()
+    assert_same(from_dev(to, ins[0], off_o), exp, dt)
+
+
 @pytest.mark.parametrize("dt,op", [(FP32, 0), (FP32, 3), (BF16, 0), (4, 1), (FP16, 2)])
 def test_reduce_out_of_place(dt, op):
     n = 32771
