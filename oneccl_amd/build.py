@@ -61,7 +61,7 @@ def build_shim(force: bool = False) -> Path:
         cxx = os.environ.get("CXX", "g++")
         _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
               "-o", str(out), str(CSRC / "comp.cpp"),
-              f"-L{LIB}", "-lmi_reduce", "-Wl,-rpath,$ORIGIN"])
+              f"-L{LIB}", "-lmi_reduce", "-ldl", "-Wl,-rpath,$ORIGIN"])
     return out
 
 

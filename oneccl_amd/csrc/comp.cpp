@@ -20,6 +20,8 @@
 //                      CCL_THROW.
 //   default          : standalone libccl_comp_hip.so for this repo's tests and
 //                      bench (ccl_mirror.hpp; same mangled symbols).
+#include <dlfcn.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -233,6 +235,47 @@ void run_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* ou
 
 int dtype_id(const ccl_datatype& dt) { return static_cast<int>(dt.idx()); }
 
+// ---- tracing ----------------------------------------------------------------
+// The reference wraps ccl_comp_reduce_regular in an ITT event of that name
+// (comp.cpp:90-93, 116-118).  The ROCm counterpart is a roctx range, which
+// `rocprofv3 --marker-trace` records next to the kernel trace.  The roctx
+// library is loaded on first use with dlopen, so the shim has no link-time
+// dependency on the profiler SDK; without it, or with MI_ROCTX=0, ranges
+// are no-ops.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+};
+
+const Roctx& roctx() {
+    static const Roctx r = [] {
+        Roctx x;
+        const char* off = getenv("MI_ROCTX");
+        if (off && strcmp(off, "0") == 0) return x;
+        for (const char* name : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                                 "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"}) {
+            void* h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (!h) continue;
+            x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+            x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+            if (x.push && x.pop) break;
+            x = Roctx();
+        }
+        return x;
+    }();
+    return r;
+}
+
+struct TraceRange {
+    const bool on;
+    explicit TraceRange(const char* name) : on(roctx().push != nullptr) {
+        if (on) roctx().push(name);
+    }
+    ~TraceRange() {
+        if (on) roctx().pop();
+    }
+};
+
 }  // namespace
 
 // ===========================================================================
@@ -311,6 +354,7 @@ static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void
     }
     const int dt = dtype_id(dtype);
     if (mi_dtype_size(dt) == 0) MI_CCL_THROW("unexpected value " + std::to_string(dt));
+    TraceRange range("comp_reduce_regular");
     if (dt == MI_BFLOAT16) {
         ccl_bf16_reduce(in_buf, in_count, inout_buf, out_count, reduction);
     } else if (dt == MI_FLOAT16) {
@@ -338,6 +382,7 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
     // The fp32 scratch `tmp`/`acc` of the reference (comp.cpp:210-234) is not
     // needed: the kernel keeps the fp32 accumulator in registers.
     const size_t es = dtype.size();
+    TraceRange range("comp_batch_reduce");
     if (bf16_keep_precision_mode) {
         // keep-precision: buffers read as bf16 whatever dtype says; inputs
         // strided by dtype.size() (comp.cpp:214-234)

@@ -470,3 +470,35 @@ def test_comp_request_free_waits_for_pending():
     req = comp.comp_reduce_start(x.data_ptr(), n, y.data_ptr(), comp.datatype.float32, comp.reduction.sum)
     req.free()
     assert bool((y == 3.5).all())
+
+
+def test_roctx_range_around_reduce(tmp_path):
+    """The ITT event the reference puts around ccl_comp_reduce_regular
+    (comp.cpp:90-93) is a roctx range here: `rocprofv3 --marker-trace` records
+    comp_reduce_regular and comp_batch_reduce ranges from the drop-in."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(prof).exists():
+        pytest.skip("rocprofv3 not installed")
+    root = Path(__file__).resolve().parent.parent
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np\n"
+            "from oneccl_amd import comp\n"
+            "a = np.ones(4096, np.float32); b = np.ones(4096, np.float32)\n"
+            "for _ in range(3): comp.comp_reduce(a.ctypes.data, a.size, b.ctypes.data, comp.datatype.float32, "
+            "comp.reduction.sum)\n"
+            "p = np.ones(3 * 64, np.float32); o = p[:64].copy()\n"
+            "comp.comp_batch_reduce(p.ctypes.data, [0, 64, 128], 64, o.ctypes.data, comp.datatype.float32, "
+            "comp.reduction.sum)\n"
+            "assert (b == 4).all() and (o == 3).all()\n") % str(root)
+    env = dict(os.environ, TMPDIR="/tmp")
+    r = subprocess.run([prof, "--marker-trace", "--output-format", "csv", "-d", str(tmp_path), "-o", "trace", "--",
+                        sys.executable, "-c", code], cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    text = "".join(p.read_text(errors="replace") for p in tmp_path.rglob("*.csv"))
+    assert text.count("comp_reduce_regular") >= 3, (r.stdout + r.stderr)[-2000:]
+    assert "comp_batch_reduce" in text
