@@ -248,6 +248,41 @@ Kern pick(int dt, int op, unsigned v) {
 }
 
 // ---------------------------------------------------------------------------
+// pointer classification
+// ---------------------------------------------------------------------------
+enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
+
+// `devptr` (optional): the device-visible address of a pinned host pointer.
+PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof(at));
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // clear the sticky "invalid value" for unregistered memory
+        return PK_PAGEABLE;
+    }
+    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) {
+        *dev = at.device;
+        return PK_DEVICE;
+    }
+    if (at.type == hipMemoryTypeHost) {
+        if (devptr) *devptr = at.devicePointer ? at.devicePointer : const_cast<void*>(p);
+        return PK_PINNED;
+    }
+    return PK_PAGEABLE;
+}
+
+// A kernel may only touch device memory or pinned host memory: a pageable
+// host pointer reaching a device entry point would fault the GPU, so it is
+// refused here instead (the *_sync entry points stage pageable memory).
+int require_gpu_visible(const void* p) {
+    int dev = -1;
+    if (classify(p, &dev) == PK_PAGEABLE)
+        return fail(MI_E_INVALID, "pageable host memory passed to a device entry point (use the *_sync form)");
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // the asynchronous core: out = fold(inputs[0..k-1]) on device pointers
 // ---------------------------------------------------------------------------
 int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
@@ -260,6 +295,10 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
     if (!out) return fail(MI_E_INVALID, "null output");
     for (int i = 0; i < k; i++)
         if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+
+    for (int i = 0; i < k; i++)
+        if (int rc = require_gpu_visible(inputs[i])) return rc;
+    if (int rc = require_gpu_visible(out)) return rc;
 
     const unsigned v = canon_flags(dt, op, flags, k);
     if (k == 1 && !(v & V_ACC_FP32)) {  // nothing to combine: result is inputs[0]
@@ -405,28 +444,6 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
         for (size_t i = 0; i < nbuf; i++) MI_HIP(hipMalloc(&d->dbuf[s][i], d->dbuf_bytes));
     }
     return 0;
-}
-
-enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
-
-// `devptr` (optional): the device-visible address of a pinned host pointer.
-PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
-    hipPointerAttribute_t at;
-    memset(&at, 0, sizeof(at));
-    hipError_t e = hipPointerGetAttributes(&at, p);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();  // clear the sticky "invalid value" for unregistered memory
-        return PK_PAGEABLE;
-    }
-    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) {
-        *dev = at.device;
-        return PK_DEVICE;
-    }
-    if (at.type == hipMemoryTypeHost) {
-        if (devptr) *devptr = at.devicePointer ? at.devicePointer : const_cast<void*>(p);
-        return PK_PINNED;
-    }
-    return PK_PAGEABLE;
 }
 
 // Issue a fold with any pointer kinds on the calling thread's streams of the
@@ -597,6 +614,8 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     if (!fn) return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
     if (count == 0) return 0;
     if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    if (int rc = require_gpu_visible(src)) return rc;
+    if (int rc = require_gpu_visible(dst)) return rc;
     CArgs a;
     memset(&a, 0, sizeof(a));
     a.src = src;
@@ -814,6 +833,8 @@ int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {
     if (bytes == 0) return 0;
     if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+    if (int rc = require_gpu_visible(src)) return rc;
+    if (int rc = require_gpu_visible(dst)) return rc;
     hipStream_t s = (hipStream_t)stream;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) == 0;
     if (!aligned) {

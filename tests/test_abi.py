@@ -112,6 +112,21 @@ def test_argument_errors_need_no_device():
     assert m.mi_reduce_multi(arr, 17, 0, 10, 9, 0, 0, None) == -1
 
 
+def test_device_entry_points_refuse_pageable_memory():
+    """A pageable host pointer handed to an asynchronous device entry point is
+    refused before any launch (a kernel touching it would fault the GPU)."""
+    m = _lib.mi()
+    a = (ctypes.c_float * 64)()
+    b = (ctypes.c_float * 64)()
+    pa, pb = ctypes.addressof(a), ctypes.addressof(b)
+    assert m.mi_reduce(pa, pb, 64, 9, 0, 0, None) == -1
+    assert b"pageable" in m.mi_last_error()
+    assert m.mi_reduce_out(pa, pb, pb, 64, 9, 0, 0, None) == -1
+    assert m.mi_reduce_multi(_lib.void_ptr_array([pa, pb, pa]), 3, pb, 64, 9, 0, 0, None) == -1
+    assert m.mi_convert(pa, 9, pb, 11, 64, 0, None) == -1
+    assert m.mi_copy(pa, pb, 256, 0, None) == -1
+
+
 @pytest.mark.parametrize("count", [0, 1, 255, 256, 1000, 1 << 28, (1 << 28) + 3])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_shard_range_partitions(count, world):

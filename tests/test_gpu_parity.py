@@ -210,6 +210,22 @@ def test_batch_reduce_keep_precision(bimpl, k, n):
     assert_same(from_dev(holders[0][0], ins[0]), exp, BF16)
 
 
+def test_pageable_pointer_refused_without_fault():
+    """Device entry points refuse pageable host memory instead of launching a
+    kernel that would fault; pinned host memory is accepted (zero-copy)."""
+    import torch
+    m = _lib.mi()
+    a = np.ones(4096, np.float32)
+    b = np.ones(4096, np.float32)
+    assert m.mi_reduce(a.ctypes.data, b.ctypes.data, a.size, FP32, 0, 0, _stream()) == -1
+    assert b"pageable" in m.mi_last_error()
+    ha = torch.ones(4096, dtype=torch.float32).pin_memory()
+    hb = torch.ones(4096, dtype=torch.float32).pin_memory()
+    _lib.check(m.mi_reduce(ha.data_ptr(), hb.data_ptr(), 4096, FP32, 0, 0, _stream()))
+    _sync()
+    assert bool((hb == 2).all())
+
+
 def test_zero_count_and_errors():
     m = _lib.mi()
     assert m.mi_reduce(0, 0, 0, FP32, 0, 0, _stream()) == 0
