@@ -836,23 +836,21 @@ int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* str
     if (int rc = require_gpu_visible(src)) return rc;
     if (int rc = require_gpu_visible(dst)) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | bytes) & 15u) == 0;
-    if (!aligned) {
-        MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
-        return 0;
-    }
-    const uint64_t nvec = bytes / 16;
+    // the destination's 16-byte grid; the source may be at any offset from it
+    const uint32_t head = (uint32_t)std::min<size_t>((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u, bytes);
+    const uint64_t nvec = (bytes - head) / 16;
+    const uint32_t tail = (uint32_t)(bytes - head - nvec * 16);
     const uint64_t tile = (uint64_t)kBlock * 4;
     uint64_t blocks = (nvec + tile - 1) / tile;
     const int cap = max_blocks();
     if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
     blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 0x7FFFFFFFull);
+    const char* s8 = static_cast<const char*>(src);
+    char* d8 = static_cast<char*>(dst);
     if (nontemporal)
-        hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
-                           static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), nvec);
+        hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
     else
-        hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
-                           static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), nvec);
+        hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
     MI_HIP(hipGetLastError());
     return 0;
 }

@@ -719,10 +719,22 @@ __global__ __launch_bounds__(kBlock) void convert_kernel(CArgs a) {
     }
 }
 
-// 16-byte vector copy with optional non-temporal stores (ccl_comp_copy).
+// Byte copy with optional non-temporal stores (ccl_comp_copy), on the
+// destination's 16-byte grid: block 0 copies the < 16-byte head and tail byte
+// by byte, the body moves 16-byte vectors.  The source may sit at any byte
+// offset from that grid (unaligned 16-byte loads, as in the reduce kernels).
 template <int MEM>
-__global__ __launch_bounds__(kBlock) void copy_kernel(const u32x4* __restrict__ src,
-                                                      u32x4* __restrict__ dst, uint64_t nvec) {
+__global__ __launch_bounds__(kBlock) void copy_kernel(const char* __restrict__ src8, char* __restrict__ dst8,
+                                                      uint32_t head, uint64_t nvec, uint32_t tail) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < head) dst8[threadIdx.x] = src8[threadIdx.x];
+        if (threadIdx.x < tail) {
+            const uint64_t o = head + nvec * 16 + threadIdx.x;
+            dst8[o] = src8[o];
+        }
+    }
+    const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(src8 + head);
+    u32x4* __restrict__ dst = reinterpret_cast<u32x4*>(dst8 + head);
     constexpr int U = 4;
     const uint64_t tile = (uint64_t)kBlock * U;
     for (uint64_t base = (uint64_t)blockIdx.x * tile + threadIdx.x; base < nvec;

@@ -215,6 +215,24 @@ def test_custom_reduction_callback():
 
 
 @pytest.mark.parametrize("nt", [0, 1])
+def test_comp_copy_any_offsets(nt):
+    """ccl_comp_copy between device buffers at every byte offset pair mod 16
+    and odd sizes: the copy kernel on the destination's 16-byte grid."""
+    import torch
+    rng = np.random.default_rng(5)
+    src = torch.from_numpy(rng.integers(0, 256, 1 << 20, dtype=np.uint8)).cuda()
+    ref = src.cpu().numpy()
+    for so in (0, 1, 3, 4, 8, 15):
+        for do in (0, 2, 5, 12):
+            for n in (1, 15, 16, 17, 4099, (1 << 19) + 3):
+                dst = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+                comp.comp_copy(src.data_ptr() + so, dst.data_ptr() + do, n, bool(nt))
+                got = dst.cpu().numpy()
+                assert np.array_equal(got[do:do + n], ref[so:so + n]), (so, do, n)
+                assert not got[:do].any() and not got[do + n:].any(), (so, do, n)
+
+
+@pytest.mark.parametrize("nt", [0, 1])
 def test_comp_copy(nt):
     import torch
     n = (5 << 20) + 3

@@ -278,10 +278,10 @@ int main(int argc, char** argv) {
         vs.push_back({mem ? "copy_kernel nt-store" : "copy_kernel plain", 2.0 * bytes, [=](hipStream_t st) {
                           if (mem)
                               hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
-                                                 (const u32x4*)in, (u32x4*)cp, nvec);
+                                                 (const char*)in, (char*)cp, 0u, nvec, 0u);
                           else
                               hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
-                                                 (const u32x4*)in, (u32x4*)cp, nvec);
+                                                 (const char*)in, (char*)cp, 0u, nvec, 0u);
                       }, {}});
     }
 
