@@ -172,7 +172,10 @@ hipError_t launch_fan(dim3, hipStream_t s, const KArgs& a) {
     constexpr int B = fan_block<Tag>();
     const uint64_t blocks = std::max<uint64_t>((a.nvec + B - 1) / B, 1);
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-    hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B>), dim3((unsigned)blocks), dim3(B), 0, s, a);
+    if (a.k <= 8)
+        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, 8>), dim3((unsigned)blocks), dim3(B), 0, s, a);
+    else
+        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, kMaxInputs>), dim3((unsigned)blocks), dim3(B), 0, s, a);
     return hipGetLastError();
 }
 

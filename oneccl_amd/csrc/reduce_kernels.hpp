@@ -578,7 +578,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, ui
 // first combine (uniform branches on k only), then the left fold in the
 // reference's order (acc = in[0]; acc = op(in[j], acc)).  Common alignment
 // required; head/tail by block 0 through the scalar element path.
-template <typename Tag, int OP, unsigned V, int B>
+template <typename Tag, int OP, unsigned V, int B, int KMAX = kMaxInputs>
 __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
@@ -597,20 +597,20 @@ __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
     // Materialise every input pointer before the first branch: left alone, the
     // compiler sinks each kernarg load into its `i < k` block and every buffer
     // load then waits on its own scalar load.
-    const void* in[kMaxInputs];
+    const void* in[KMAX];
 #pragma unroll
-    for (int i = 0; i < kMaxInputs; i++) {
+    for (int i = 0; i < KMAX; i++) {
         in[i] = a.in[i];
         asm volatile("" ::"s"(in[i]));
     }
-    u32x4 x[kMaxInputs];
+    u32x4 x[KMAX];
 #pragma unroll
-    for (int i = 0; i < kMaxInputs; i++)
+    for (int i = 0; i < KMAX; i++)
         if (i < k) x[i] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], byte0, bytes), off, 0, kAuxNT);
     if constexpr (packed_int<Tag>()) {
         u32x4 r = x[0];
 #pragma unroll
-        for (int i = 1; i < kMaxInputs; i++)
+        for (int i = 1; i < KMAX; i++)
             if (i < k) r = pk_op4<Tag, OP>(x[i], r);
         __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
         return;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
 #pragma unroll
     for (int e = 0; e < N; e++) acc[e] = widen<Tag>(p0.e[e]);
 #pragma unroll
-    for (int i = 1; i < kMaxInputs; i++) {
+    for (int i = 1; i < KMAX; i++) {
         if (i < k) {
             const Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i]);
 #pragma unroll
