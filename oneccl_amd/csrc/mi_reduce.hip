@@ -625,9 +625,15 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     a.dst = dst;
     a.count = count;
     a.trunc_from = trunc_from;
+    // vector path on dst's 16-byte grid (as launch_reduce): both pointers
+    // aligned to their element size; the source may sit at any such offset
+    const size_t ss = dtype_size(sdt), ds = dtype_size(ddt);
     const uintptr_t sa = reinterpret_cast<uintptr_t>(src), da = reinterpret_cast<uintptr_t>(dst);
-    a.scalar_only = ((sa | da) & 15u) ? 1 : 0;  // vector path: 16-byte aligned src and dst
-    a.ngroups = a.scalar_only ? 0 : count / 8;
+    const bool same = (sa & 15u) == 0 && (da & 15u) == 0;
+    const bool vec = (sa % ss) == 0 && (da % ds) == 0 && (same || unaligned_vectors());
+    a.scalar_only = vec ? 0 : 1;
+    a.head = vec ? std::min<uint64_t>(((16 - (da & 15u)) & 15u) / ds, count) : 0;
+    a.ngroups = vec ? (count - a.head) / 8 : 0;
     const uint64_t work = a.scalar_only ? count : std::max<uint64_t>(a.ngroups, 1);
     uint64_t blocks = std::min<uint64_t>((work + kBlock - 1) / kBlock, 1u << 20);
     blocks = std::max<uint64_t>(blocks, 1);

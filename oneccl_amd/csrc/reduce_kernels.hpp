@@ -670,6 +670,7 @@ struct CArgs {
     const void* src;
     void* dst;
     uint64_t count;       // elements
+    uint64_t head;        // elements before dst's first 16-byte boundary (vector path)
     uint64_t ngroups;     // groups of 8 elements on the vector path
     uint64_t trunc_from;  // V_TAIL_TRUNC: elements >= trunc_from truncate
     int scalar_only;
@@ -696,26 +697,34 @@ __global__ __launch_bounds__(kBlock) void convert_kernel(CArgs a) {
             static_cast<DS*>(a.dst)[i] = convert_elem<ST, DT, V>(static_cast<const SS*>(a.src)[i], i, a.trunc_from);
         return;
     }
+    // vector body on dst's 16-byte grid from element `head` on; the source
+    // vectors may be unaligned (element-aligned loads of 16 bytes)
     constexpr int SV = 8 * sizeof(SS) / 16;  // 16-byte source vectors per group
     constexpr int DV = 8 * sizeof(DS) / 16;
+    const u32x4* src = reinterpret_cast<const u32x4*>(static_cast<const SS*>(a.src) + a.head);
+    u32x4* dst = reinterpret_cast<u32x4*>(static_cast<DS*>(a.dst) + a.head);
     for (; i < a.ngroups; i += stride) {
         Pack<SS> sp[SV];
 #pragma unroll
-        for (int v = 0; v < SV; v++)
-            sp[v] = __builtin_bit_cast(Pack<SS>, vload<3>(static_cast<const u32x4*>(a.src) + i * SV + v));
+        for (int v = 0; v < SV; v++) sp[v] = __builtin_bit_cast(Pack<SS>, vload<3>(src + i * SV + v));
         Pack<DS> dp[DV];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             constexpr int SN = 16 / sizeof(SS), DN = 16 / sizeof(DS);
-            dp[e / DN].e[e % DN] = convert_elem<ST, DT, V>(sp[e / SN].e[e % SN], i * 8 + e, a.trunc_from);
+            dp[e / DN].e[e % DN] = convert_elem<ST, DT, V>(sp[e / SN].e[e % SN], a.head + i * 8 + e, a.trunc_from);
         }
 #pragma unroll
-        for (int v = 0; v < DV; v++) vstore<3>(static_cast<u32x4*>(a.dst) + i * DV + v, __builtin_bit_cast(u32x4, dp[v]));
+        for (int v = 0; v < DV; v++) vstore<3>(dst + i * DV + v, __builtin_bit_cast(u32x4, dp[v]));
     }
-    // tail (count % 8 elements) by the first lanes of block 0
-    if (blockIdx.x == 0 && threadIdx.x < a.count - a.ngroups * 8) {
-        const uint64_t j = a.ngroups * 8 + threadIdx.x;
-        static_cast<DS*>(a.dst)[j] = convert_elem<ST, DT, V>(static_cast<const SS*>(a.src)[j], j, a.trunc_from);
+    // head (< 16 bytes of dst) and tail (< 8 elements) by the first lanes of block 0
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.head)
+            static_cast<DS*>(a.dst)[threadIdx.x] =
+                convert_elem<ST, DT, V>(static_cast<const SS*>(a.src)[threadIdx.x], threadIdx.x, a.trunc_from);
+        if (threadIdx.x < a.count - a.head - a.ngroups * 8) {
+            const uint64_t j = a.head + a.ngroups * 8 + threadIdx.x;
+            static_cast<DS*>(a.dst)[j] = convert_elem<ST, DT, V>(static_cast<const SS*>(a.src)[j], j, a.trunc_from);
+        }
     }
 }
 

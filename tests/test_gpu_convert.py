@@ -104,6 +104,44 @@ def test_convert_unaligned(offs):
     assert_same(got, oracle.f32_to_fp16(src), FP16)
 
 
+CONV_PAIRS = [(FP32, BF16, comp.F_BF16_RNE | comp.F_BF16_TAIL_TRUNC16), (FP32, BF16, 0), (FP32, FP16, 0),
+              (BF16, FP32, 0), (FP16, FP32, 0)]
+
+
+@pytest.mark.parametrize("sdt,ddt,flags", CONV_PAIRS, ids=["f32-bf16rne-tail", "f32-bf16trunc", "f32-f16",
+                                                           "bf16-f32", "f16-f32"])
+@pytest.mark.parametrize("offs", [(0, 0), (1, 0), (0, 1), (3, 5), (2, 7)])
+@pytest.mark.parametrize("vectors", [1, 0], ids=["unaligned-vectors", "element-loop"])
+def test_convert_any_offsets(sdt, ddt, flags, offs, vectors):
+    """Conversions between sub-buffers at any element offsets: the vector path
+    on dst's 16-byte grid (scalar head, unaligned source vectors, tail) and the
+    element loop give the oracle's bits, including the count % 16 truncated
+    tail of ccl_convert_fp32_to_bf16_arrays (bf16.cpp:145-148)."""
+    n = 8 * 4099 + 13
+    rng = np.random.default_rng(sum(offs) + 10 * sdt + ddt)
+    f = (rng.standard_normal(n) * 7).astype(np.float32)
+    if sdt == FP32:
+        src = f
+        exp = np.empty(n, np.uint16)
+        if ddt == BF16:
+            impl = 2 if flags else 0
+            oracle.lib().orc_convert_fp32_to_bf16_arrays(src.ctypes.data, exp.ctypes.data, n, impl)
+        else:
+            exp = oracle.f32_to_fp16(src)
+        out_dtype = np.uint16
+    else:
+        src = oracle.f32_to_bf16(f, True) if sdt == BF16 else oracle.f32_to_fp16(f)
+        exp = oracle.bf16_to_f32(src) if sdt == BF16 else oracle.fp16_to_f32(src)
+        out_dtype = np.float32
+    m = _lib.mi()
+    prev = m.mi_set_unaligned_vectors(vectors)
+    try:
+        got = _gpu_convert(src, sdt, ddt, flags, out_dtype, *offs)
+    finally:
+        m.mi_set_unaligned_vectors(prev)
+    assert_same(got, exp, ddt)
+
+
 def test_fp16_vector_entry_points():
     src = np.array([1.0, -2.5, 65504.0, 1e-7, 65520.0, -0.0, 3.14159, 1e5], np.float32)
     h = np.zeros(8, np.uint16)
