@@ -15,7 +15,7 @@ import pytest
 import oracle
 from oneccl_amd import _lib, comp
 from tests import kat
-from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, FP32, OP_NAME, OPS, assert_same, from_dev, rand_array, to_dev
+from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, FP32, FP64, OP_NAME, OPS, assert_same, from_dev, rand_array, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -85,6 +85,35 @@ def test_comp_reduce_pointer_kinds(where, dt):
         got = b.copy()
         comp.comp_reduce(pa, n, ptr(got), comp.datatype(dt), comp.reduction.sum)
     assert_same(got, exp, dt, where)
+
+
+@pytest.mark.parametrize("dt,off_in,off_io", [(FP32, 1, 0), (BF16, 3, 6), (0, 5, 2), (FP64, 0, 1), (FP16, 7, 7)])
+@pytest.mark.parametrize("mode", [0, 1], ids=["zero_copy", "staged"])
+def test_pinned_host_differing_offsets(dt, off_in, off_io, mode):
+    """Sub-buffers of pinned staging memory at element offsets whose
+    addresses differ mod 16: the zero-copy kernel reads them over PCIe with
+    unaligned 16-byte loads; the staged pipeline copies them first."""
+    import torch
+    n = (3 << 20) + 17
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=71, specials=False)
+    b = rand_array(dt, n, seed=72, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce(a, exp, dt, 0, b_impl, f_impl)
+    es = a.itemsize
+    ha = torch.zeros((n + 16) * es, dtype=torch.uint8).pin_memory()
+    hb = torch.zeros((n + 16) * es, dtype=torch.uint8).pin_memory()
+    ha.numpy()[off_in * es:(off_in + n) * es] = a.view(np.uint8)
+    hb.numpy()[off_io * es:(off_io + n) * es] = b.view(np.uint8)
+    m = _lib.mi()
+    prev = m.mi_set_host_mode(mode)
+    try:
+        comp.comp_reduce(ha.data_ptr() + off_in * es, n, hb.data_ptr() + off_io * es, comp.datatype(dt),
+                         comp.reduction.sum)
+    finally:
+        m.mi_set_host_mode(prev)
+    got = hb.numpy()[off_io * es:(off_io + n) * es].view(b.dtype)
+    assert_same(got, exp, dt)
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["zero_copy", "staged"])
