@@ -61,6 +61,11 @@ struct ccl_comp_request;
 int mi_ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf,
                              size_t* out_count, int dtype, int op, mi_ccl_reduction_fn fn,
                              struct ccl_comp_request** req);
+/* ccl_comp_batch_reduce_start: the fused K-input fold as one request. */
+int mi_ccl_comp_batch_reduce_start(const void* in_buf, const size_t* offsets, size_t n_offsets,
+                                   size_t in_count, void* inout_buf, size_t* out_count, int dtype,
+                                   int op, int bf16_keep_precision_mode,
+                                   struct ccl_comp_request** req);
 int mi_ccl_comp_request_test(struct ccl_comp_request* req, int* done);
 int mi_ccl_comp_request_wait(struct ccl_comp_request* req);
 int mi_ccl_comp_request_free(struct ccl_comp_request* req);

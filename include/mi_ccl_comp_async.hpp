@@ -30,6 +30,7 @@
 #define MI_CCL_COMP_ASYNC_HPP
 
 #include <cstddef>
+#include <vector>
 
 struct ccl_comp_request;  // opaque; one per started reduce
 
@@ -39,6 +40,17 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
                                   size_t* out_count, const ccl_datatype& dtype,
                                   ccl::reduction reduction, ccl::reduction_fn reduction_fn,
                                   const ccl::fn_context* context, ccl_comp_request** req);
+
+/* The same for ccl_comp_batch_reduce (src/comp/comp.cpp:202-249): the fused
+ * K-input fold of in_buf + offsets[i] * dtype.size() into inout_buf, as one
+ * request (several chained launches past 16 inputs).  The fp32 scratch
+ * `tmp` / `acc` of the synchronous form is not needed and not taken.     */
+ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<size_t>& offsets,
+                                        size_t in_count, void* inout_buf, size_t* out_count,
+                                        const ccl_datatype& dtype, ccl::reduction reduction,
+                                        ccl::reduction_fn reduction_fn,
+                                        const ccl::fn_context* context,
+                                        int bf16_keep_precision_mode, ccl_comp_request** req);
 
 /* true once inout_buf holds the result and both buffers may be reused. */
 bool ccl_comp_request_test(ccl_comp_request* req);

@@ -80,6 +80,8 @@ SHIM_API = [
     ("mi_ccl_convert_fp16_to_fp32", c_int, [c_void_p, c_void_p]),
     ("mi_ccl_comp_reduce_start", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int, c_int,
                                          MI_CCL_REDUCTION_FN, POINTER(c_void_p)]),
+    ("mi_ccl_comp_batch_reduce_start", c_int, [c_void_p, POINTER(c_size_t), c_size_t, c_size_t, c_void_p,
+                                               POINTER(c_size_t), c_int, c_int, c_int, POINTER(c_void_p)]),
     ("mi_ccl_comp_request_test", c_int, [c_void_p, POINTER(c_int)]),
     ("mi_ccl_comp_request_wait", c_int, [c_void_p]),
     ("mi_ccl_comp_request_free", c_int, [c_void_p]),

@@ -217,6 +217,18 @@ def comp_reduce_start(in_ptr: int, count: int, inout_ptr: int, dtype: datatype, 
     return comp_request(h.value, None if oc.value == 0xFFFFFFFFFFFFFFFF else oc.value, cb)
 
 
+def comp_batch_reduce_start(in_ptr: int, offsets: Sequence[int], count: int, inout_ptr: int, dtype: datatype,
+                            op: reduction, bf16_keep_precision_mode: int = 0) -> comp_request:
+    """ccl_comp_batch_reduce_start: the fused K-input fold as one request."""
+    offs = (ctypes.c_size_t * len(offsets))(*offsets)
+    oc = ctypes.c_size_t(0xFFFFFFFFFFFFFFFF)
+    h = ctypes.c_void_p()
+    check_shim(shim().mi_ccl_comp_batch_reduce_start(in_ptr, offs, len(offsets), count, inout_ptr, ctypes.byref(oc),
+                                                     int(dtype), int(op), int(bf16_keep_precision_mode),
+                                                     ctypes.byref(h)), "ccl_comp_batch_reduce_start")
+    return comp_request(h.value, None if oc.value == 0xFFFFFFFFFFFFFFFF else oc.value)
+
+
 def comp_copy(in_ptr: int, out_ptr: int, nbytes: int, use_nontemporal: bool = False) -> None:
     check_shim(shim().mi_ccl_comp_copy(in_ptr, out_ptr, nbytes, int(use_nontemporal)), "ccl_comp_copy")
 
@@ -243,6 +255,6 @@ def shard_range(count: int, rank: int, world: int, align: int = 256) -> tuple[in
 
 
 __all__ = ["reduction", "datatype", "bf16_impl", "fp16_impl", "reduce", "reduce_out", "reduce_multi",
-           "comp_reduce", "comp_reduce_start", "comp_request", "comp_batch_reduce", "comp_copy", "reduction_to_str", "impl_types", "env_reload",
+           "comp_reduce", "comp_reduce_start", "comp_batch_reduce_start", "comp_request", "comp_batch_reduce", "comp_copy", "reduction_to_str", "impl_types", "env_reload",
            "shard_range", "bf16_flags", "fp16_flags", "reference_flags", "F_MINMAX_INOUT_FIRST", "F_BF16_RNE",
            "F_ACC_FP32", "F_BF16_TAIL_TRUNC16", "DTYPE_SIZE", "_lib"]

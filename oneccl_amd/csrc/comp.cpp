@@ -374,15 +374,19 @@ ccl::status ccl_comp_reduce(ccl_sched* /*sched*/, const void* in_buf, size_t in_
     return comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
 }
 
-ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
-                                  void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
-                                  ccl::reduction reduction, ccl::reduction_fn reduction_fn,
-                                  const ccl::fn_context* context, int bf16_keep_precision_mode, float* /*tmp*/,
-                                  float* /*acc*/) {
+// ccl_comp_batch_reduce's body, with the issue of each fused fold (`issue(ins,
+// k, out, count, dtype, op, flags)`) left to the caller: synchronous
+// (mi_reduce_multi_sync) or asynchronous (mi_reduce_start, one request per
+// group of <= 16 inputs; the groups of one call land on the calling thread's
+// streams in order, so they chain).
+template <typename Issue>
+static void batch_reduce_body(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
+                              void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
+                              ccl::reduction reduction, ccl::reduction_fn reduction_fn,
+                              const ccl::fn_context* context, int bf16_keep_precision_mode, Issue&& issue) {
     // The fp32 scratch `tmp`/`acc` of the reference (comp.cpp:210-234) is not
     // needed: the kernel keeps the fp32 accumulator in registers.
     const size_t es = dtype.size();
-    TraceRange range("comp_batch_reduce");
     if (bf16_keep_precision_mode) {
         // keep-precision: buffers read as bf16 whatever dtype says; inputs
         // strided by dtype.size() (comp.cpp:214-234)
@@ -390,7 +394,7 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
             MI_CCL_THROW("custom reduction is not supported in bf16 keep-precision mode");
         const size_t k = std::max<size_t>(offsets.size(), 1);
         if (k > MI_MAX_INPUTS) MI_CCL_THROW("keep-precision fan-in supports at most 16 inputs");
-        if (in_count == 0) return ccl::status::success;
+        if (in_count == 0) return;
         std::vector<const void*> ins(k);
         ins[0] = inout_buf;
         for (size_t i = 1; i < k; i++) ins[i] = static_cast<const char*>(in_buf) + es * offsets[i];
@@ -399,26 +403,20 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
         // avx512f / scalar truncate all (bf16.cpp:130-149)
         unsigned f = MI_F_ACC_FP32;
         if (mi_bf16_impl() == ccl_bf16_avx512bf) f |= MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16;
-        check(mi_reduce_multi_sync(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16,
-                                   static_cast<int>(reduction), f, mi_comp_device()),
-              "mi_reduce_multi_sync");
-        return ccl::status::success;
+        issue(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16, static_cast<int>(reduction), f);
+        return;
     }
-    if (offsets.size() <= 1 || in_count == 0) return ccl::status::success;
+    if (offsets.size() <= 1 || in_count == 0) return;
     if (reduction == ccl::reduction::custom) {
         for (size_t i = 1; i < offsets.size(); i++)
             comp_reduce_regular(static_cast<const char*>(in_buf) + es * offsets[i], in_count, inout_buf, out_count,
                                 dtype, reduction, reduction_fn, context);
-        return ccl::status::success;
+        return;
     }
     // storage-precision left fold == the reference's chained reduces
     const int dt = dtype_id(dtype);
     unsigned f = 0;
-    if (dt == MI_BFLOAT16) {
-        f = bf16_flags(mi_bf16_impl());
-    } else if (dt == MI_FLOAT16) {
-        if (!fp16_flags(mi_fp16_impl(), &f)) return ccl::status::success;
-    }
+    if (!reduce_semantics(dt, &f)) return;
     if ((dt == MI_BFLOAT16 || dt == MI_FLOAT16) && out_count) *out_count = in_count;
     size_t next = 1;
     while (next < offsets.size()) {
@@ -427,9 +425,22 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
         ins[k++] = inout_buf;
         while (next < offsets.size() && k < MI_MAX_INPUTS)
             ins[k++] = static_cast<const char*>(in_buf) + es * offsets[next++];
-        check(mi_reduce_multi_sync(ins, k, inout_buf, in_count, dt, static_cast<int>(reduction), f, mi_comp_device()),
-              "mi_reduce_multi_sync");
+        issue(ins, k, inout_buf, in_count, dt, static_cast<int>(reduction), f);
     }
+}
+
+ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
+                                  void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
+                                  ccl::reduction reduction, ccl::reduction_fn reduction_fn,
+                                  const ccl::fn_context* context, int bf16_keep_precision_mode, float* /*tmp*/,
+                                  float* /*acc*/) {
+    TraceRange range("comp_batch_reduce");
+    batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
+                      bf16_keep_precision_mode,
+                      [](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
+                          check(mi_reduce_multi_sync(ins, k, out, n, dt, op, f, mi_comp_device()),
+                                "mi_reduce_multi_sync");
+                      });
     return ccl::status::success;
 }
 
@@ -437,7 +448,7 @@ const char* ccl_reduction_to_str(ccl::reduction type) { return mi_reduction_to_s
 
 // ---- asynchronous ccl_comp_reduce (include/mi_ccl_comp_async.hpp) --------
 struct ccl_comp_request {
-    mi_request_t r = nullptr;  // null: completed inside start (empty, custom, fp16 no-op)
+    std::vector<mi_request_t> r;  // empty: completed inside start (empty, custom, fp16 no-op)
 };
 
 ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
@@ -456,9 +467,11 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
             unsigned f = 0;
             if (reduce_semantics(dt, &f)) {
                 const void* ins[2] = {inout_buf, in_buf};
+                mi_request_t r = nullptr;
                 check(mi_reduce_start(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f,
-                                      mi_comp_device(), &q->r),
+                                      mi_comp_device(), &r),
                       "mi_reduce_start");
+                q->r.push_back(r);
             }
         }
     }
@@ -466,32 +479,63 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
     return ccl::status::success;
 }
 
+ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
+                                        void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
+                                        ccl::reduction reduction, ccl::reduction_fn reduction_fn,
+                                        const ccl::fn_context* context, int bf16_keep_precision_mode,
+                                        ccl_comp_request** req) {
+    if (!req) MI_CCL_THROW("null request pointer");
+    *req = nullptr;
+    std::unique_ptr<ccl_comp_request> q(new ccl_comp_request());
+    struct Drop {  // on a throw, wait for and release what was already issued
+        ccl_comp_request* q;
+        ~Drop() {
+            if (!q) return;
+            for (mi_request_t r : q->r) {
+                (void)mi_wait(r);
+                (void)mi_request_free(r);
+            }
+        }
+    } drop{q.get()};
+    batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
+                      bf16_keep_precision_mode,
+                      [&](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
+                          mi_request_t r = nullptr;
+                          check(mi_reduce_start(ins, k, out, n, dt, op, f, mi_comp_device(), &r), "mi_reduce_start");
+                          q->r.push_back(r);
+                      });
+    drop.q = nullptr;
+    *req = q.release();
+    return ccl::status::success;
+}
+
 bool ccl_comp_request_test(ccl_comp_request* req) {
     if (!req) MI_CCL_THROW("null request");
-    if (!req->r) return true;
-    int done = 0;
-    check(mi_test(req->r, &done), "mi_test");
-    return done != 0;
+    for (mi_request_t r : req->r) {  // groups complete in issue order
+        int done = 0;
+        check(mi_test(r, &done), "mi_test");
+        if (!done) return false;
+    }
+    return true;
 }
 
 void ccl_comp_request_wait(ccl_comp_request* req) {
     if (!req) MI_CCL_THROW("null request");
-    if (req->r) check(mi_wait(req->r), "mi_wait");
+    for (mi_request_t r : req->r) check(mi_wait(r), "mi_wait");
 }
 
 // Waits first if the request is still pending: freeing must never leave a
 // kernel writing into a buffer its owner already considers free.
 void ccl_comp_request_free(ccl_comp_request* req) {
     if (!req) return;
-    if (req->r) {
-        const int rc = mi_wait(req->r);
-        (void)mi_request_free(req->r);
-        req->r = nullptr;
-        delete req;
-        check(rc, "mi_wait");
-        return;
+    int rc = 0;
+    for (mi_request_t r : req->r) {
+        const int w = mi_wait(r);
+        if (w && !rc) rc = w;
+        (void)mi_request_free(r);
     }
     delete req;
+    check(rc, "mi_wait");
 }
 
 #ifndef MI_ONECCL_TREE
@@ -587,6 +631,17 @@ int mi_ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_bu
     MI_SHIM_GUARD(return (int)ccl_comp_reduce_start(in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
                                                     static_cast<ccl::reduction>(op),
                                                     reinterpret_cast<ccl::reduction_fn>(fn), nullptr, req));
+}
+
+int mi_ccl_comp_batch_reduce_start(const void* in_buf, const size_t* offsets, size_t n_offsets, size_t in_count,
+                                   void* inout_buf, size_t* out_count, int dtype, int op,
+                                   int bf16_keep_precision_mode, struct ccl_comp_request** req) {
+    MI_SHIM_GUARD({
+        std::vector<size_t> offs(offsets, offsets + n_offsets);
+        return (int)ccl_comp_batch_reduce_start(in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                                static_cast<ccl::reduction>(op), nullptr, nullptr,
+                                                bf16_keep_precision_mode, req);
+    });
 }
 
 int mi_ccl_comp_request_test(struct ccl_comp_request* req, int* done) {

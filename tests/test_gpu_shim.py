@@ -549,3 +549,33 @@ def test_roctx_range_around_reduce(tmp_path):
     text = "".join(p.read_text(errors="replace") for p in tmp_path.rglob("*.csv"))
     assert text.count("comp_reduce_regular") >= 3, (r.stdout + r.stderr)[-2000:]
     assert "comp_batch_reduce" in text
+
+
+@pytest.mark.parametrize("where", ["device", "pageable"])
+@pytest.mark.parametrize("dt,op,k,keep", [(FP32, 0, 5, 0), (FP32, 3, 23, 0), (BF16, 0, 4, 1), (BF16, 2, 9, 0),
+                                          (4, 1, 17, 0), (FP16, 0, 3, 0)])
+def test_comp_batch_reduce_start_matches_sync(where, dt, op, k, keep):
+    """ccl_comp_batch_reduce_start (one request; chained launches past 16
+    inputs) gives the bits and out_count of the synchronous
+    ccl_comp_batch_reduce, which the parity suite pins to the oracle."""
+    n = 40_001
+    es = oracle.NP_DTYPE[dt]().itemsize
+    packed = np.concatenate([rand_array(dt, n, seed=500 + j + 37 * dt, op=op) for j in range(k)])
+    offs = [j * n for j in range(k)]
+    ref = packed[:n].copy()
+    oc_ref = comp.comp_batch_reduce(ptr(packed), offs, n, ptr(ref), comp.datatype(dt), comp.reduction(op), keep)
+    if where == "device":
+        tp, pp = to_dev(packed)
+        to, po = to_dev(packed[:n].copy())
+    else:
+        host = packed[:n].copy()
+        pp, po = ptr(packed), ptr(host)
+    req = comp.comp_batch_reduce_start(pp, offs, n, po, comp.datatype(dt), comp.reduction(op), keep)
+    try:
+        _poll(req)
+    finally:
+        req.free()
+    got = from_dev(to, ref) if where == "device" else host
+    assert_same(got, ref, dt)
+    assert req.out_count == oc_ref
+    assert es == ref.itemsize
