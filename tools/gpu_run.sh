@@ -80,13 +80,15 @@ for step in "$@"; do
                 > "$GRAFT_REPO_ROOT/$OUT/proftrace.out" 2> "$GRAFT_REPO_ROOT/$OUT/proftrace.err")
             rc=$?; echo "=== proftrace rc=$rc" | tee -a "$OUT/steps.log"
             [ $rc -eq 0 ] || exit $rc ;;
-        pmc)
+        pmc)  # PMC_CONFIG=c4 etc. counts another bench config (output under pmc_<config>/)
+            pc=${PMC_CONFIG:-c2}; pdir=$OUT; [ "$pc" = c2 ] || pdir=$OUT/pmc_$pc
+            mkdir -p "$pdir"
             for ctr in FETCH_SIZE WRITE_SIZE; do
                 (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv \
-                    -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o bench -- \
-                    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-host-leg \
-                    > "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err")
-                rc=$?; echo "=== pmc $ctr rc=$rc" | tee -a "$OUT/steps.log"
+                    -d "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr" -o bench -- \
+                    python3 "$GRAFT_REPO_ROOT/bench.py" --config "$pc" --steps 5 --warmup 2 --no-cpu-baseline \
+                    --no-host-leg > "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.err")
+                rc=$?; echo "=== pmc $pc $ctr rc=$rc" | tee -a "$OUT/steps.log"
                 [ $rc -eq 0 ] || exit $rc
             done ;;
         *) echo "unknown step $step"; exit 2 ;;

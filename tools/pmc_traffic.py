@@ -19,7 +19,7 @@ import sys
 from pathlib import Path
 
 
-def kernel_values(path: Path, needles=("reduce2_kernel", "reduce_kernel")) -> list[float]:
+def kernel_values(path: Path, needles=("reduce2_kernel", "reduce_kernel", "fan_kernel")) -> list[float]:
     rows = list(csv.DictReader(open(path)))
     return [float(r["Counter_Value"]) for r in rows if any(n in r["Kernel_Name"] for n in needles)]
 
