@@ -579,3 +579,56 @@ def test_comp_batch_reduce_start_matches_sync(where, dt, op, k, keep):
     assert_same(got, ref, dt)
     assert req.out_count == oc_ref
     assert es == ref.itemsize
+
+
+def test_concurrent_worker_stress():
+    """16 worker threads (CCL_WORKER_COUNT-style), each running 40 reduces that
+    mix pointer kinds (device, pinned, pageable), dtypes, ops, synchronous and
+    asynchronous entry points and fused fan-ins, concurrently; every result
+    checked against the oracle."""
+    import threading
+
+    import torch
+    b_impl, f_impl = impls()
+    errs = []
+    n = 33_333
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(t)
+            for it in range(40):
+                dt = [FP32, BF16, FP16, 4, 6, 0][int(rng.integers(0, 6))]
+                op = int(rng.integers(0, 4))
+                a = rand_array(dt, n, seed=1000 * t + it, op=op, specials=False)
+                b = rand_array(dt, n, seed=1000 * t + it + 500, op=op, specials=False)
+                exp = b.copy()
+                oracle.comp_reduce(a, exp, dt, op, b_impl, f_impl)
+                kind = int(rng.integers(0, 3))
+                if kind == 0:
+                    ta, pa = to_dev(a)
+                    tb, pb = to_dev(b)
+                elif kind == 1:
+                    ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+                    hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+                    pa, pb = ha.data_ptr(), hb.data_ptr()
+                else:
+                    hbuf = b.copy()
+                    pa, pb = ptr(a), ptr(hbuf)
+                if rng.random() < 0.5:
+                    comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction(op))
+                else:
+                    req = comp.comp_reduce_start(pa, n, pb, comp.datatype(dt), comp.reduction(op))
+                    req.wait()
+                    req.free()
+                got = from_dev(tb, b) if kind == 0 else (hb.numpy().view(b.dtype) if kind == 1 else hbuf)
+                assert_same(got, exp, dt, f"thread {t} iter {it} kind {kind}")
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=240)
+    assert not any(x.is_alive() for x in th), "a worker did not finish"
+    assert not errs, errs[:3]
