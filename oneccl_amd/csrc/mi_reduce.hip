@@ -7,7 +7,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -398,6 +401,8 @@ struct DevCtx {
     hipStream_t stream[2] = {nullptr, nullptr};
     std::vector<void*> dbuf[2];  // per pipeline slot: one device buffer per host operand
     size_t dbuf_bytes = 0;
+    hipStream_t d2h = nullptr;              // the drain thread's stream (created on first use)
+    hipEvent_t ready[2] = {nullptr, nullptr};  // per slot: the chunk's result is in dbuf
 
     ~DevCtx() {
         // Contexts die with their thread; device teardown at process exit may
@@ -405,8 +410,84 @@ struct DevCtx {
         for (int s = 0; s < 2; s++) {
             for (void* p : dbuf[s]) (void)hipFree(p);
             if (stream[s]) (void)hipStreamDestroy(stream[s]);
+            if (ready[s]) (void)hipEventDestroy(ready[s]);
+        }
+        if (d2h) (void)hipStreamDestroy(d2h);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// drain thread for staged results bound for pageable host memory
+// ---------------------------------------------------------------------------
+// A D2H copy into pageable memory blocks the thread that issues it until the
+// copy is done.  Issued inline, chunk c's D2H therefore sits between chunk
+// c's kernel and chunk c+1's H2D, and the staged pipeline uses one PCIe
+// direction at a time (17 GiB/s for a 256 MiB bucket).  On a helper thread it
+// runs while the calling thread copies the next chunk in, so both directions
+// are busy.  Used by the synchronous entry points only; the helper exists for
+// the duration of one call.
+struct Drain {
+    struct Task {
+        void* dst;
+        const void* src;
+        size_t bytes;
+        hipEvent_t ready;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Task> q;
+    size_t done = 0;  // tasks finished (or skipped after an error)
+    bool stop = false;
+    hipError_t err = hipSuccess;
+    std::thread th;
+
+    void start(int device, hipStream_t s) {
+        if (th.joinable()) return;
+        th = std::thread([this, device, s] { loop(device, s); });
+    }
+    void loop(int device, hipStream_t s) {
+        hipError_t e = hipSetDevice(device);
+        for (;;) {
+            Task t;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                t = q.front();
+                q.pop_front();
+            }
+            if (e == hipSuccess) e = hipEventSynchronize(t.ready);
+            if (e == hipSuccess) e = hipMemcpyAsync(t.dst, t.src, t.bytes, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            std::lock_guard<std::mutex> lk(mu);
+            if (e != hipSuccess && err == hipSuccess) err = e;
+            done++;
+            cv.notify_all();
         }
     }
+    void push(const Task& t) {
+        std::lock_guard<std::mutex> lk(mu);
+        q.push_back(t);
+        cv.notify_all();
+    }
+    // wait until `n` tasks are finished; the first error of the helper, if any
+    hipError_t wait_done(size_t n) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done >= n; });
+        return err;
+    }
+    hipError_t finish() {
+        if (th.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            th.join();
+        }
+        return err;
+    }
+    ~Drain() { (void)finish(); }
 };
 
 struct ThreadCtx {
@@ -455,7 +536,7 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
 // Otherwise: chunks of kChunkBytes, two pipeline slots on two streams (H2D
 // of chunk c+1 overlaps the kernel / D2H of chunk c).
 int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
-                 unsigned flags, int device, DevCtx** ctx, int* used) {
+                 unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr) {
     *ctx = nullptr;
     *used = 0;
     const size_t es = dtype_size(dt);
@@ -543,9 +624,18 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
 
     const size_t nchunks = (count + chunk_elems - 1) / chunk_elems;
     *used = nchunks > 1 ? 3 : 1;
+    const bool drained = drain && kout == PK_PAGEABLE && slot_of[k] >= 0 && nchunks > 1;
+    if (drained) {
+        if (!d->d2h) MI_HIP(hipStreamCreateWithFlags(&d->d2h, hipStreamNonBlocking));
+        for (int s = 0; s < 2; s++)
+            if (!d->ready[s]) MI_HIP(hipEventCreateWithFlags(&d->ready[s], hipEventDisableTiming));
+        drain->start(d->device, d->d2h);
+    }
     for (size_t c = 0; c < nchunks; c++) {
         const int s = (int)(c & 1);
         hipStream_t st = d->stream[s];
+        // slot s holds chunk c-2's result until the helper has copied it out
+        if (drained && c >= 2) MI_HIP(drain->wait_done(c - 1));
         const size_t off = c * chunk_elems;
         const size_t n = std::min(chunk_elems, count - off);
         const size_t bytes = n * es;
@@ -571,8 +661,14 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         // launch_reduce is the same split.
         rc = launch_reduce(din, k, dout, n, dt, op, flags, st);
         if (rc) return rc;
-        if (slot_of[k] >= 0)
-            MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, dout, bytes, hipMemcpyDeviceToHost, st));
+        if (slot_of[k] >= 0) {
+            if (drained) {
+                MI_HIP(hipEventRecord(d->ready[s], st));
+                drain->push({static_cast<char*>(out) + off * es, dout, bytes, d->ready[s]});
+            } else {
+                MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, dout, bytes, hipMemcpyDeviceToHost, st));
+            }
+        }
     }
     return 0;
 }
@@ -581,8 +677,11 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
                 unsigned flags, int device) {
     DevCtx* d = nullptr;
     int used = 0;
-    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used);
+    Drain drain;
+    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain);
+    const hipError_t de = drain.finish();  // every staged result is in `out` after this
     if (rc) return rc;
+    if (de != hipSuccess) return hip_fail(de, "staged D2H into pageable memory");
     for (int s = 0; s < 2; s++)
         if (used & (1 << s)) MI_HIP(wait_stream(d->stream[s]));
     return 0;
