@@ -140,8 +140,10 @@ int mi_reduce_multi_sync(const void* const* inputs, int k, void* out,
  * final), mi_wait blocks, mi_request_free releases it (after completion).
  * Lets a schedule entry return `started` and poll from update() instead of
  * blocking its worker thread (reduce_local_entry.cpp:
- * 116-135 polls the Level Zero path the same way).  Pageable host operands
- * are staged by copies that may block inside mi_reduce_start.            */
+ * 116-135 polls the Level Zero path the same way).  Work that needs host
+ * staging (pageable operands) runs on a worker thread owned by the calling
+ * thread, in submission order, so mi_reduce_start returns at once for it
+ * too.  mi_request_free waits for a request that is still running.       */
 typedef struct mi_request* mi_request_t;
 int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count,
                     int dtype, int op, unsigned flags, int device,

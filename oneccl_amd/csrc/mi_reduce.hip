@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
+#include <memory>
 #include <thread>
 #include <cstdlib>
 #include <cstring>
@@ -688,6 +689,96 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
 }
 
 // ---------------------------------------------------------------------------
+// asynchronous staging: a worker thread per calling thread
+// ---------------------------------------------------------------------------
+// The runtime's copies to and from pageable memory are host-synchronous, so an
+// mi_reduce_start that staged pageable operands inline would return only when
+// the copies were done, and a schedule entry polling it would gain nothing.
+// Requests that need staging go instead to a worker thread owned by the
+// calling thread. It runs them in submission order through the synchronous
+// pipeline (drain thread included), with its own streams and staging buffers
+// that persist across requests.
+struct AsyncJob {
+    const void* inputs[MI_MAX_INPUTS];
+    int k = 0;
+    void* out = nullptr;
+    size_t count = 0;
+    int dt = 0, op = 0;
+    unsigned flags = 0;
+    int device = -1;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    int rc = 0;
+    std::string err;
+
+    int wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done; });
+        return rc;
+    }
+};
+
+struct StageWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::shared_ptr<AsyncJob>> q;
+    bool stop = false;
+
+    void submit(const std::shared_ptr<AsyncJob>& j) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(j);
+        }
+        if (!th.joinable()) th = std::thread([this] { loop(); });
+        cv.notify_all();
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<AsyncJob> j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;
+                j = q.front();
+                q.pop_front();
+            }
+            const int rc = reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags, j->device);
+            std::lock_guard<std::mutex> lk(j->mu);
+            j->rc = rc;
+            if (rc) j->err = g_last_error;  // the worker's thread-local message
+            j->done = true;
+            j->cv.notify_all();
+        }
+    }
+    // Thread exit: finish every submitted job (they write the callers'
+    // buffers), then stop.
+    ~StageWorker() {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+};
+thread_local StageWorker t_stage;
+
+// Does a fold over these operands need host staging (pageable operands, or
+// pinned ones under MI_HOST_STAGED)?
+bool needs_staging(const void* const* inputs, int k, const void* out) {
+    const bool staged_mode = host_mode() == MI_HOST_STAGED;
+    for (int i = 0; i <= k; i++) {
+        int dev = -1;
+        const PtrKind kind = classify(i < k ? inputs[i] : out, &dev);
+        if (kind == PK_PAGEABLE || (kind == PK_PINNED && staged_mode)) return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
 // conversions
 // ---------------------------------------------------------------------------
 typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&);
@@ -845,6 +936,7 @@ struct mi_request {
     hipEvent_t ev[2] = {nullptr, nullptr};
     int nev = 0;
     int device = -1;
+    std::shared_ptr<AsyncJob> job;  // staged work running on the calling thread's worker
 };
 
 int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
@@ -852,6 +944,31 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
     if (!req) return fail(MI_E_INVALID, "null request pointer");
     *req = nullptr;
     if (!inputs) return fail(MI_E_INVALID, "null input list");
+    if (!dtype_size(dtype)) return fail(MI_E_INVALID, "unknown datatype");
+    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+    if (count > 0) {
+        if (!out) return fail(MI_E_INVALID, "null output");
+        for (int i = 0; i < k; i++)
+            if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+        if (op < MI_OP_SUM || op > MI_OP_MAX)
+            return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
+        if (needs_staging(inputs, k, out)) {
+            auto j = std::make_shared<AsyncJob>();
+            for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
+            j->k = k;
+            j->out = out;
+            j->count = count;
+            j->dt = dtype;
+            j->op = op;
+            j->flags = flags;
+            j->device = device;
+            t_stage.submit(j);
+            mi_request* r = new mi_request();
+            r->job = j;
+            *req = r;
+            return 0;
+        }
+    }
     DevCtx* d = nullptr;
     int used = 0;
     int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used);
@@ -881,6 +998,12 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
 
 int mi_test(mi_request_t req, int* done) {
     if (!req || !done) return fail(MI_E_INVALID, "null request");
+    if (req->job) {
+        std::lock_guard<std::mutex> lk(req->job->mu);
+        *done = req->job->done ? 1 : 0;
+        if (req->job->done && req->job->rc) return fail(req->job->rc, req->job->err.c_str());
+        return 0;
+    }
     *done = 1;
     for (int i = 0; i < req->nev; i++) {
         const hipError_t e = hipEventQuery(req->ev[i]);
@@ -896,12 +1019,17 @@ int mi_test(mi_request_t req, int* done) {
 
 int mi_wait(mi_request_t req) {
     if (!req) return fail(MI_E_INVALID, "null request");
+    if (req->job) {
+        const int rc = req->job->wait();
+        return rc ? fail(rc, req->job->err.c_str()) : 0;
+    }
     for (int i = 0; i < req->nev; i++) MI_HIP(hipEventSynchronize(req->ev[i]));
     return 0;
 }
 
 int mi_request_free(mi_request_t req) {
     if (!req) return 0;
+    if (req->job) (void)req->job->wait();  // the job writes the caller's buffers: never leave it running
     for (int i = 0; i < req->nev; i++)
         if (req->ev[i]) (void)hipEventDestroy(req->ev[i]);
     delete req;

@@ -146,3 +146,43 @@ def test_hipgraph_capture_and_replay():
     torch.cuda.synchronize()
     assert_same(from_dev(tb, b), exp_b, FP32)
     assert_same(from_dev(td, d), exp_d, BF16)
+
+
+def test_pageable_start_returns_before_the_work_is_done():
+    """mi_reduce_start on pageable operands hands the staged pipeline to the
+    calling thread's worker and returns at once; requests run in submission
+    order, so a request that reads the previous one's output sees it."""
+    import time
+    m = _lib.mi()
+    n = (256 << 20) // 4
+    a = rand_array(FP32, n, seed=11, specials=False)
+    b = rand_array(FP32, n, seed=12, specials=False)
+    c = rand_array(FP32, n, seed=13, specials=False)
+    exp_b = b.copy()
+    oracle.comp_reduce_mt(a, exp_b, FP32, 0, 8)
+    exp_c = c.copy()
+    oracle.comp_reduce_mt(exp_b, exp_c, FP32, 0, 8)
+    # warm the worker (its streams and staging buffers) with one small request
+    w = np.ones(1 << 20, np.float32)
+    req = ctypes.c_void_p()
+    _lib.check(m.mi_reduce_start(_lib.void_ptr_array([w.ctypes.data, w.ctypes.data]), 2, w.ctypes.data, w.size,
+                                 FP32, 0, 0, -1, ctypes.byref(req)))
+    _lib.check(m.mi_request_free(req))
+    t0 = time.perf_counter()
+    r1, r2 = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.check(m.mi_reduce_start(_lib.void_ptr_array([b.ctypes.data, a.ctypes.data]), 2, b.ctypes.data, n, FP32, 0,
+                                 0, -1, ctypes.byref(r1)))
+    _lib.check(m.mi_reduce_start(_lib.void_ptr_array([c.ctypes.data, b.ctypes.data]), 2, c.ctypes.data, n, FP32, 0,
+                                 0, -1, ctypes.byref(r2)))
+    t_start = time.perf_counter() - t0
+    done = ctypes.c_int(0)
+    _lib.check(m.mi_test(r2, ctypes.byref(done)))
+    assert done.value == 0  # 2 x 256 MiB staged over PCIe cannot be done yet
+    _lib.check(m.mi_wait(r1))
+    _lib.check(m.mi_wait(r2))
+    t_all = time.perf_counter() - t0
+    _lib.check(m.mi_request_free(r1))
+    _lib.check(m.mi_request_free(r2))
+    assert_same(b, exp_b, FP32, "first request")
+    assert_same(c, exp_c, FP32, "second request reads the first one's output")
+    assert t_start < 0.25 * t_all, (t_start, t_all)

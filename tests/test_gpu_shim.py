@@ -255,6 +255,7 @@ def test_comp_copy_any_offsets(nt):
         for do in (0, 2, 5, 12):
             for n in (1, 15, 16, 17, 4099, (1 << 19) + 3):
                 dst = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()  # the fill runs on torch's stream, the copy on the library's
                 comp.comp_copy(src.data_ptr() + so, dst.data_ptr() + do, n, bool(nt))
                 got = dst.cpu().numpy()
                 assert np.array_equal(got[do:do + n], ref[so:so + n]), (so, do, n)
@@ -270,8 +271,9 @@ def test_comp_copy(nt):
     comp.comp_copy(ptr(src), ptr(dst), n, bool(nt))
     assert np.array_equal(src, dst)
     td = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    comp.comp_copy(ptr(src), td.data_ptr(), n, bool(nt))
     td2 = torch.zeros_like(td)
+    torch.cuda.synchronize()  # the fills run on torch's stream, the copies on the library's
+    comp.comp_copy(ptr(src), td.data_ptr(), n, bool(nt))
     comp.comp_copy(td.data_ptr(), td2.data_ptr(), n - 16, bool(nt))
     comp.comp_copy(td.data_ptr() + n - 16, td2.data_ptr() + n - 16, 16, bool(nt))
     assert np.array_equal(td2.cpu().numpy(), src)
