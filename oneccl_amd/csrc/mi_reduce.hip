@@ -404,6 +404,8 @@ struct DevCtx {
     size_t dbuf_bytes = 0;
     hipStream_t d2h = nullptr;              // the drain thread's stream (created on first use)
     hipEvent_t ready[2] = {nullptr, nullptr};  // per slot: the chunk's result is in dbuf
+    std::vector<void*> hbuf;                // pinned bounce buffers for small pageable operands
+    size_t hbuf_bytes = 0;
 
     ~DevCtx() {
         // Contexts die with their thread; device teardown at process exit may
@@ -414,6 +416,7 @@ struct DevCtx {
             if (ready[s]) (void)hipEventDestroy(ready[s]);
         }
         if (d2h) (void)hipStreamDestroy(d2h);
+        for (void* p : hbuf) (void)hipHostFree(p);
     }
 };
 
@@ -516,6 +519,22 @@ int get_ctx(int device, DevCtx** out) {
     return 0;
 }
 
+// Small pageable operands are copied through pinned bounce buffers by the
+// CPU and reduced by the zero-copy kernel: below about 1 MiB the runtime's
+// pageable copies cost more than the data (profiles/round1_size_sweep*.jsonl).
+constexpr size_t kBounceBytes = 1ull << 20;  // per operand
+
+int ensure_bounce(DevCtx* d, size_t nbuf) {
+    if (d->hbuf.size() >= nbuf) return 0;
+    while (d->hbuf.size() < nbuf) {
+        void* p = nullptr;
+        MI_HIP(hipHostMalloc(&p, kBounceBytes, hipHostMallocDefault));
+        d->hbuf.push_back(p);
+    }
+    d->hbuf_bytes = kBounceBytes;
+    return 0;
+}
+
 int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
     if (d->dbuf[0].size() >= nbuf && d->dbuf_bytes >= bytes) return 0;
     for (int s = 0; s < 2; s++) {
@@ -536,8 +555,16 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
 // bit 1: stream[1]).  All-device or zero-copy: one launch on stream[0].
 // Otherwise: chunks of kChunkBytes, two pipeline slots on two streams (H2D
 // of chunk c+1 overlaps the kernel / D2H of chunk c).
+// A copy the synchronous caller makes after the GPU is done (bounce -> `out`).
+struct HostCopy {
+    void* dst = nullptr;
+    const void* src = nullptr;
+    size_t bytes = 0;
+};
+
 int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
-                 unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr) {
+                 unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr,
+                 HostCopy* post = nullptr) {
     *ctx = nullptr;
     *used = 0;
     const size_t es = dtype_size(dt);
@@ -599,6 +626,34 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     if (all_dev || direct) {
         *used = 1;
         return launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
+    }
+
+    // small pageable operands (synchronous callers only): CPU copy into
+    // pinned bounce buffers, zero-copy kernel, CPU copy of the result back
+    bool any_pageable = kout == PK_PAGEABLE;
+    for (int i = 0; i < k; i++) any_pageable = any_pageable || kin[i] == PK_PAGEABLE;
+    if (post && any_pageable && host_mode() == MI_HOST_AUTO && count * es <= kBounceBytes) {
+        const void* bins[MI_MAX_INPUTS];
+        const void* bsrc[MI_MAX_INPUTS + 1];
+        void* bbuf[MI_MAX_INPUTS + 1];
+        int nb = 0;
+        auto bounce_of = [&](const void* p, bool copy_in) -> void* {
+            for (int j = 0; j < nb; j++)
+                if (bsrc[j] == p) return bbuf[j];
+            bsrc[nb] = p;
+            bbuf[nb] = d->hbuf[nb];
+            if (copy_in) memcpy(bbuf[nb], p, count * es);
+            return bbuf[nb++];
+        };
+        rc = ensure_bounce(d, (size_t)k + 1);
+        if (rc) return rc;
+        for (int i = 0; i < k; i++) bins[i] = kin[i] == PK_PAGEABLE ? bounce_of(inputs[i], true) : dins[i];
+        void* bout = kout == PK_PAGEABLE ? bounce_of(out, false) : dout;
+        *used = 1;
+        rc = launch_reduce(bins, k, bout, count, dt, op, flags, d->stream[0]);
+        if (rc) return rc;
+        if (kout == PK_PAGEABLE) *post = HostCopy{out, bout, count * es};
+        return 0;
     }
 
     // distinct host operands get a device staging buffer per slot; `out`
@@ -679,12 +734,14 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     DevCtx* d = nullptr;
     int used = 0;
     Drain drain;
-    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain);
+    HostCopy post;
+    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain, &post);
     const hipError_t de = drain.finish();  // every staged result is in `out` after this
     if (rc) return rc;
     if (de != hipSuccess) return hip_fail(de, "staged D2H into pageable memory");
     for (int s = 0; s < 2; s++)
         if (used & (1 << s)) MI_HIP(wait_stream(d->stream[s]));
+    if (post.bytes) memcpy(post.dst, post.src, post.bytes);
     return 0;
 }
 

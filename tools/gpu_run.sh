@@ -30,7 +30,7 @@ for step in "$@"; do
         tests_fast)
             run pytest_gpu 600 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider -k "not full" ;;
         asan)
-            ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 run asan 300 ./tests/cpp/dropin_caller_asan ;;
+            ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0 run asan 300 ./tests/cpp/dropin_caller_asan ;;
         latency)
             run latency 300 ./tools/latency 2000 ;;
         smoke)
