@@ -639,3 +639,19 @@ def test_concurrent_worker_stress():
         x.join(timeout=240)
     assert not any(x.is_alive() for x in th), "a worker did not finish"
     assert not errs, errs[:3]
+
+
+@pytest.mark.parametrize("k", [3, 16, 17])
+@pytest.mark.parametrize("n", [1000, 70_001, (3 << 20) // 4 + 5])
+@pytest.mark.parametrize("dt,op", [(FP32, 0), (BF16, 3), (0, 1)])
+def test_batch_reduce_pageable_vs_oracle(k, n, dt, op):
+    """ccl_comp_batch_reduce on pageable host memory (oneCCL's tmp buffer
+    holding the peers' chunks): small buckets through the pinned bounce
+    buffers, larger ones through the staged pipeline; chained past 16 inputs."""
+    b_impl, f_impl = impls()
+    ins = [rand_array(dt, n, seed=40 + 3 * j + dt, op=op) for j in range(k)]
+    exp = oracle.fanin(ins, dt, op, b_impl, f_impl)
+    packed = np.concatenate(ins)
+    io = ins[0].copy()
+    comp.comp_batch_reduce(ptr(packed), [j * n for j in range(k)], n, ptr(io), comp.datatype(dt), comp.reduction(op))
+    assert_same(io, exp, dt)
