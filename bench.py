@@ -346,6 +346,30 @@ def host_resident_leg(m, dt, es, op, flags, n):
             m.mi_host_unregister(pb)
     m.mi_set_host_mode(0)
     res["register_ms_two_buffers"] = round(reg_s * 1e3, 2) if reg_s is not None else None
+    # several GPUs in one node: one pageable bucket split by element range over
+    # all of them (mi_reduce_multi_sync_sharded), each shard over its own link
+    ndev = torch.cuda.device_count()
+    if ndev > 1:
+        try:
+            import ctypes
+            from oneccl_amd import _lib
+            nn = n * ndev
+            a = np.zeros(nn * es, np.uint8)
+            b = np.zeros(nn * es, np.uint8)
+            arr = _lib.void_ptr_array([b.ctypes.data, a.ctypes.data])
+            devs = (ctypes.c_int * ndev)(*range(ndev))
+            times = []
+            for i in range(4):
+                t0 = time.perf_counter()
+                rc = m.mi_reduce_multi_sync_sharded(arr, 2, b.ctypes.data, nn, dt, op, flags, ndev, devs)
+                if rc:
+                    raise RuntimeError(m.mi_last_error().decode())
+                if i:
+                    times.append(time.perf_counter() - t0)
+            res["pageable_all_gpus"] = {"value": round(nn * es / GiB / min(times), 3), "gpus": ndev,
+                                        "bucket_bytes": nn * es}
+        except Exception as e:  # noqa: BLE001 — an extra leg never breaks the bench line
+            res["pageable_all_gpus"] = {"error": str(e)}
     return {"unit": "GiB/s bucket incl. both operands host->GPU and the result GPU->host over PCIe",
             "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync",
             "modes": "pinned = zero-copy kernel on pinned host memory (default); pinned_staged = chunked "

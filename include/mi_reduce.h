@@ -157,6 +157,16 @@ int mi_request_free(mi_request_t req);
  * HIP device devices[s] — all pointers of a shard live on its device.  Every
  * shard is launched before any is waited for; no inter-GPU traffic, no
  * collective.  Synchronous.                                                */
+/* One bucket of any pointer kinds split by element range over `nshards`
+ * GPUs (devices[s] may repeat), every shard reduced at once: shard 0 on the
+ * calling thread, the others on worker threads it owns.  For host-resident
+ * buckets each GPU moves its shard over its own PCIe link, so the
+ * PCIe-inclusive rate adds up over GPUs.  Synchronous; same bits as
+ * mi_reduce_multi_sync (shard boundaries are 256-element aligned).        */
+int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, size_t count,
+                                 int dtype, int op, unsigned flags, int nshards,
+                                 const int* devices);
+
 int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs,
                       int k, void* const* outs, const size_t* counts, int dtype,
                       int op, unsigned flags);

@@ -46,6 +46,8 @@ MI_API = [
     ("mi_request_free", c_int, [c_void_p]),
     ("mi_reduce_sharded", c_int, [c_int, POINTER(c_int), POINTER(c_void_p), c_int, POINTER(c_void_p),
                                   POINTER(c_size_t), c_int, c_int, c_uint]),
+    ("mi_reduce_multi_sync_sharded", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint,
+                                             c_int, POINTER(c_int)]),
     ("mi_copy_sync", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int]),
     ("mi_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("mi_shard_range", c_int, [c_size_t, c_int, c_int, c_size_t, POINTER(c_size_t), POINTER(c_size_t)]),

@@ -1093,6 +1093,50 @@ int mi_request_free(mi_request_t req) {
     return 0;
 }
 
+// ---- one bucket split over several GPUs, any pointer kinds -----------------
+int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                                 unsigned flags, int nshards, const int* devices) {
+    if (!inputs || !devices || nshards < 1) return fail(MI_E_INVALID, "bad shard arguments");
+    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+    const size_t es = dtype_size(dtype);
+    if (!es) return fail(MI_E_INVALID, "unknown datatype");
+    if (nshards == 1 || count == 0) return reduce_sync(inputs, k, out, count, dtype, op, flags, devices[0]);
+    // Shards start on 256-element boundaries, so the bf16 count % 16 tail
+    // (MI_F_BF16_TAIL_TRUNC16) lies in the last shard exactly as in the
+    // whole array.  Shard 0 runs on the calling thread, the others on
+    // workers owned by it (one per shard slot, persistent streams/staging).
+    thread_local std::vector<std::unique_ptr<StageWorker>> t_shard_workers;
+    while ((int)t_shard_workers.size() < nshards - 1) t_shard_workers.emplace_back(new StageWorker());
+    const size_t per = ((count + (size_t)nshards - 1) / (size_t)nshards + 255) / 256 * 256;
+    std::vector<std::shared_ptr<AsyncJob>> jobs;
+    for (int sh = 1; sh < nshards; sh++) {
+        const size_t b = std::min(count, per * (size_t)sh), e = std::min(count, b + per);
+        if (b >= e) break;
+        auto j = std::make_shared<AsyncJob>();
+        for (int i = 0; i < k; i++) j->inputs[i] = static_cast<const char*>(inputs[i]) + b * es;
+        j->k = k;
+        j->out = static_cast<char*>(out) + b * es;
+        j->count = e - b;
+        j->dt = dtype;
+        j->op = op;
+        j->flags = flags;
+        j->device = devices[sh];
+        t_shard_workers[sh - 1]->submit(j);
+        jobs.push_back(j);
+    }
+    const int rc0 = reduce_sync(inputs, k, out, std::min(count, per), dtype, op, flags, devices[0]);
+    std::string err0 = rc0 ? g_last_error : std::string();
+    int rc = rc0;
+    for (auto& j : jobs) {
+        const int r = j->wait();  // every shard finishes before the call returns
+        if (r && !rc) {
+            rc = r;
+            err0 = j->err;
+        }
+    }
+    return rc ? fail(rc, err0.c_str()) : 0;
+}
+
 // ---- in-process multi-GPU element-range shards -------------------------------
 int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs, int k, void* const* outs,
                       const size_t* counts, int dtype, int op, unsigned flags) {

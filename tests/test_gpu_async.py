@@ -186,3 +186,45 @@ def test_pageable_start_returns_before_the_work_is_done():
     assert_same(b, exp_b, FP32, "first request")
     assert_same(c, exp_c, FP32, "second request reads the first one's output")
     assert t_start < 0.25 * t_all, (t_start, t_all)
+
+
+@pytest.mark.parametrize("where", ["device", "pinned", "pageable", "pageable_small"])
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_multi_sync_sharded_same_bits(where, nshards):
+    """mi_reduce_multi_sync_sharded splits one bucket over several GPUs (here
+    the one GPU listed several times, each shard on its own thread, streams
+    and staging buffers): same bits as one call, including the bf16
+    fp32-accumulate fan-in's count % 16 truncated tail, which must fall in the
+    last shard as in the whole array."""
+    import torch
+    m = _lib.mi()
+    n = ((70 << 20) // 2 + 13) if where != "pageable_small" else 100_003
+    k = 4
+    ins = [rand_array(BF16, n, seed=60 + j, specials=False) for j in range(k)]
+    flags = 0x4 | 0x2 | 0x8  # MI_F_ACC_FP32 | MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16
+    # ccl_comp_batch_reduce(keep precision) under avx512bf, restated by the oracle
+    ref_out = ins[0].copy()
+    oracle.batch_reduce(np.concatenate(ins), [j * n for j in range(k)], n, ref_out, BF16, 0, 1,
+                        oracle.BF16_AVX512BF, 0)
+    if where == "device":
+        hs = [to_dev(x) for x in ins]
+        ptrs = [p for _, p in hs]
+        to, po = to_dev(np.zeros(n, np.uint16))
+    elif where == "pinned":
+        hs = [torch.from_numpy(x.view(np.uint8).copy()).pin_memory() for x in ins]
+        ptrs = [h.data_ptr() for h in hs]
+        ho = torch.zeros(n * 2, dtype=torch.uint8).pin_memory()
+        po = ho.data_ptr()
+    else:
+        ptrs = [x.ctypes.data for x in ins]
+        out = np.zeros(n, np.uint16)
+        po = out.ctypes.data
+    devs = (ctypes.c_int * nshards)(*([0] * nshards))
+    _lib.check(m.mi_reduce_multi_sync_sharded(_lib.void_ptr_array(ptrs), k, po, n, BF16, 0, flags, nshards, devs))
+    if where == "device":
+        got = from_dev(to, ref_out)
+    elif where == "pinned":
+        got = ho.numpy().view(np.uint16)
+    else:
+        got = out
+    assert_same(got, ref_out, BF16, f"{where} x{nshards}")
