@@ -266,6 +266,57 @@ const Roctx& roctx() {
     return r;
 }
 
+// CCL_COMP_HIP_SHARD_DEVICES=<d0>,<d1>,...: host-resident reduces are split by
+// element range over these GPUs, each shard over its own PCIe link
+// (mi_reduce_multi_sync_sharded).  Unset or one device: a single GPU.
+std::mutex g_shard_mu;
+std::vector<int> g_shard_devs;
+bool g_shard_ready = false;
+
+std::vector<int> shard_devices() {
+    std::lock_guard<std::mutex> g(g_shard_mu);
+    if (!g_shard_ready) {
+        g_shard_devs.clear();
+        if (const char* v = getenv("CCL_COMP_HIP_SHARD_DEVICES")) {
+            std::string cur;
+            for (const char* c = v;; c++) {
+                if (*c == ',' || *c == 0) {
+                    if (!cur.empty()) g_shard_devs.push_back(atoi(cur.c_str()));
+                    cur.clear();
+                    if (!*c) break;
+                } else {
+                    cur += *c;
+                }
+            }
+        }
+        g_shard_ready = true;
+    }
+    return g_shard_devs;
+}
+
+void shard_env_reload() {
+    std::lock_guard<std::mutex> g(g_shard_mu);
+    g_shard_ready = false;
+}
+
+// The synchronous fold every entry point ends in: one GPU, or, for host
+// operands under CCL_COMP_HIP_SHARD_DEVICES, several.
+int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags) {
+    const std::vector<int> devs = shard_devices();
+    if (devs.size() >= 2) {
+        bool host = !is_device_ptr(out);
+        for (int i = 0; i < k && host; i++) host = !is_device_ptr(ins[i]);
+        if (host)
+            return mi_reduce_multi_sync_sharded(ins, k, out, count, dt, op, flags, (int)devs.size(), devs.data());
+    }
+    return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+}
+
+int reduce2_sync(const void* in, void* inout, size_t count, int dt, int op, unsigned flags) {
+    const void* ins[2] = {inout, in};
+    return fold_sync(ins, 2, inout, count, dt, op, flags);
+}
+
 struct TraceRange {
     const bool on;
     explicit TraceRange(const char* name) : on(roctx().push != nullptr) {
@@ -293,8 +344,7 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
 void ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
     if (out_cnt != nullptr) *out_cnt = in_cnt;
     if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
-    check(mi_reduce_sync(in_buf, inout_buf, in_cnt, MI_BFLOAT16, static_cast<int>(op),
-                         bf16_flags(mi_bf16_impl()), mi_comp_device()),
+    check(reduce2_sync(in_buf, inout_buf, in_cnt, MI_BFLOAT16, static_cast<int>(op), bf16_flags(mi_bf16_impl())),
           "mi_reduce_sync(bf16)");
 }
 
@@ -303,8 +353,7 @@ void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t*
     if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
     unsigned f = 0;
     if (!fp16_flags(mi_fp16_impl(), &f)) return;
-    check(mi_reduce_sync(in_buf, inout_buf, in_cnt, MI_FLOAT16, static_cast<int>(op), f, mi_comp_device()),
-          "mi_reduce_sync(fp16)");
+    check(reduce2_sync(in_buf, inout_buf, in_cnt, MI_FLOAT16, static_cast<int>(op), f), "mi_reduce_sync(fp16)");
 }
 
 // ---- conversions: bf16.cpp:113-169, fp16.cpp:55-61 ------------------------
@@ -361,8 +410,7 @@ static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void
         ccl_fp16_reduce(in_buf, in_count, inout_buf, out_count, reduction);
     } else {
         // CCL_REDUCE: std::min/std::max operand order, no out_count write
-        check(mi_reduce_sync(in_buf, inout_buf, in_count, dt, static_cast<int>(reduction), 0u, mi_comp_device()),
-              "mi_reduce_sync");
+        check(reduce2_sync(in_buf, inout_buf, in_count, dt, static_cast<int>(reduction), 0u), "mi_reduce_sync");
     }
     return ccl::status::success;
 }
@@ -438,8 +486,7 @@ ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>&
     batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
                       bf16_keep_precision_mode,
                       [](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
-                          check(mi_reduce_multi_sync(ins, k, out, n, dt, op, f, mi_comp_device()),
-                                "mi_reduce_multi_sync");
+                          check(fold_sync(ins, k, out, n, dt, op, f), "mi_reduce_multi_sync");
                       });
     return ccl::status::success;
 }
@@ -672,6 +719,7 @@ int mi_ccl_env_reload(void) {
     MI_SHIM_GUARD({
         std::lock_guard<std::mutex> g(g_env_mu);
         parse_env_locked();
+        shard_env_reload();
         return 0;
     });
 }

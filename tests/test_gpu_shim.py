@@ -655,3 +655,46 @@ def test_batch_reduce_pageable_vs_oracle(k, n, dt, op):
     io = ins[0].copy()
     comp.comp_batch_reduce(ptr(packed), [j * n for j in range(k)], n, ptr(io), comp.datatype(dt), comp.reduction(op))
     assert_same(io, exp, dt)
+
+
+@pytest.mark.parametrize("dt", [FP32, BF16, 4])
+def test_shard_devices_env(dt):
+    """CCL_COMP_HIP_SHARD_DEVICES splits host-resident reduces over the listed
+    GPUs (here the one GPU twice and three times): same bits on pageable,
+    pinned and device buffers (device operands never shard), and through the
+    fused batch reduce."""
+    import os
+
+    import torch
+    b_impl, f_impl = impls()
+    n = (6 << 20) // 4 + 77
+    for devs in ("0,0", "0,0,0"):
+        os.environ["CCL_COMP_HIP_SHARD_DEVICES"] = devs
+        comp.env_reload()
+        try:
+            a = rand_array(dt, n, seed=5, specials=False)
+            b = rand_array(dt, n, seed=6, specials=False)
+            exp = b.copy()
+            oracle.comp_reduce(a, exp, dt, 0, b_impl, f_impl)
+            got = b.copy()
+            comp.comp_reduce(ptr(a), n, ptr(got), comp.datatype(dt), comp.reduction.sum)
+            assert_same(got, exp, dt, f"pageable {devs}")
+            ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+            hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+            comp.comp_reduce(ha.data_ptr(), n, hb.data_ptr(), comp.datatype(dt), comp.reduction.sum)
+            assert_same(hb.numpy().view(b.dtype), exp, dt, f"pinned {devs}")
+            ta, pa = to_dev(a)
+            tb, pb = to_dev(b)
+            comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+            assert_same(from_dev(tb, b), exp, dt, f"device {devs}")
+            k = 5
+            ins = [rand_array(dt, n, seed=70 + j, specials=False) for j in range(k)]
+            fexp = oracle.fanin(ins, dt, 0, b_impl, f_impl)
+            packed = np.concatenate(ins)
+            io = ins[0].copy()
+            comp.comp_batch_reduce(ptr(packed), [j * n for j in range(k)], n, ptr(io), comp.datatype(dt),
+                                   comp.reduction.sum)
+            assert_same(io, fexp, dt, f"batch {devs}")
+        finally:
+            os.environ.pop("CCL_COMP_HIP_SHARD_DEVICES", None)
+            comp.env_reload()
