@@ -347,34 +347,49 @@ def host_resident_leg(m, dt, es, op, flags, n):
     m.mi_set_host_mode(0)
     res["register_ms_two_buffers"] = round(reg_s * 1e3, 2) if reg_s is not None else None
     # several GPUs in one node: one pageable bucket split by element range over
-    # all of them (mi_reduce_multi_sync_sharded), each shard over its own link
-    ndev = torch.cuda.device_count()
-    if ndev > 1:
+    # all of them (mi_reduce_multi_sync_sharded), each shard over its own link.
+    # Measured in a child process under a time limit: an extra leg never
+    # breaks or stalls the bench line.
+    if torch.cuda.device_count() > 1:
+        import subprocess
         try:
-            import ctypes
-            from oneccl_amd import _lib
-            nn = n * ndev
-            a = np.zeros(nn * es, np.uint8)
-            b = np.zeros(nn * es, np.uint8)
-            arr = _lib.void_ptr_array([b.ctypes.data, a.ctypes.data])
-            devs = (ctypes.c_int * ndev)(*range(ndev))
-            times = []
-            for i in range(4):
-                t0 = time.perf_counter()
-                rc = m.mi_reduce_multi_sync_sharded(arr, 2, b.ctypes.data, nn, dt, op, flags, ndev, devs)
-                if rc:
-                    raise RuntimeError(m.mi_last_error().decode())
-                if i:
-                    times.append(time.perf_counter() - t0)
-            res["pageable_all_gpus"] = {"value": round(nn * es / GiB / min(times), 3), "gpus": ndev,
-                                        "bucket_bytes": nn * es}
-        except Exception as e:  # noqa: BLE001 — an extra leg never breaks the bench line
+            r = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--host-shard-probe", str(n), str(dt),
+                                str(es), str(op), str(flags)], capture_output=True, text=True, timeout=180)
+            res["pageable_all_gpus"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
+                "error": r.stderr[-300:]}
+        except Exception as e:  # noqa: BLE001
             res["pageable_all_gpus"] = {"error": str(e)}
     return {"unit": "GiB/s bucket incl. both operands host->GPU and the result GPU->host over PCIe",
             "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync",
             "modes": "pinned = zero-copy kernel on pinned host memory (default); pinned_staged = chunked "
                      "H2D/kernel/D2H over two streams; pageable = staged; pageable_registered = pageable buffers "
                      "registered once with mi_host_register (cost in register_ms_two_buffers), then zero-copy"}
+
+
+def host_shard_probe(n, dt, es, op, flags):
+    """Child-process leg: a pageable bucket of n elements per GPU, split over
+    every GPU of the node by mi_reduce_multi_sync_sharded; prints one JSON."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from oneccl_amd import _lib
+    m = _lib.mi()
+    ndev = torch.cuda.device_count()
+    nn = n * ndev
+    a = np.zeros(nn * es, np.uint8)
+    b = np.zeros(nn * es, np.uint8)
+    arr = _lib.void_ptr_array([b.ctypes.data, a.ctypes.data])
+    devs = (ctypes.c_int * ndev)(*range(ndev))
+    times = []
+    for i in range(4):
+        t0 = time.perf_counter()
+        _lib.check(m.mi_reduce_multi_sync_sharded(arr, 2, b.ctypes.data, nn, dt, op, flags, ndev, devs))
+        if i:
+            times.append(time.perf_counter() - t0)
+    print(json.dumps({"value": round(nn * es / GiB / min(times), 3), "unit": "GiB/s", "gpus": ndev,
+                      "bucket_bytes": nn * es, "entry": "mi_reduce_multi_sync_sharded"}), flush=True)
 
 
 def pmc_traffic(config):
@@ -391,4 +406,7 @@ def pmc_traffic(config):
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 7 and sys.argv[1] == "--host-shard-probe":
+        host_shard_probe(*(int(x) for x in sys.argv[2:]))
+    else:
+        main()
