@@ -62,6 +62,10 @@ for step in "$@"; do
                 --master-port 29534 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --scaling strong ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
+        sizes_fp32)
+            run sizes 300 python tools/size_sweep.py --configs fp32-sum ;;
+        misalign)
+            run misalign 300 python tools/misalign_probe.py ;;
         benchall)
             for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
