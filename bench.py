@@ -38,6 +38,9 @@ CONFIGS = {
                 256 << 20, 0x1),
     "c4": ("8-input fan-in fp32 sum (ring-chunk arrival pattern), 1 GiB bucket (configs[3])", 9, 4, 0, 8, GiB, 0),
     "c4-bf16acc": ("8-input fan-in bf16 sum, fp32 accumulate, 1 GiB bucket", 11, 2, 0, 8, GiB, 0x4 | 0x2),
+    "c4-tmpbuf": ("8-input fan-in fp32 sum, 1 GiB bucket, nreduce layout: the 7 peer chunks in consecutive slots of "
+                  "one tmp allocation, folded into the separate reduce_buf in place (allreduce.cpp:333-394)",
+                  9, 4, 0, 8, GiB, 0),
     "c5-int32-max": ("2-input int32 max, 1 GiB bucket (configs[4])", 4, 4, 3, 2, GiB, 0),
     "c5-int64-prod": ("2-input int64 prod, 1 GiB bucket (configs[4])", 6, 8, 1, 2, GiB, 0),
 }
@@ -190,7 +193,11 @@ def main():
 
     m = _lib.mi()
     tdt = torch_dtype(dt)
-    ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+    if args.config == "c4-tmpbuf":  # reduce_buf + one tmp buffer holding the k-1 peer chunks
+        tmp = torch.empty((k - 1) * n, dtype=tdt, device="cuda")
+        ins = [torch.empty(n, dtype=tdt, device="cuda")] + [tmp[j * n:(j + 1) * n] for j in range(k - 1)]
+    else:
+        ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
     for j, t in enumerate(ins):
         fill(t, 0xC0FFEE + 7919 * rank + j)
     stream = torch.cuda.current_stream()
