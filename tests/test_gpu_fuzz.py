@@ -8,6 +8,8 @@ The case list is fixed by the seed, so a failure names a reproducible case.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -18,7 +20,7 @@ from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, OP_NAME, OPS, assert_sam
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 1000
+N_CASES = int(os.environ.get("MI_FUZZ_CASES", "1000"))  # a longer sweep: MI_FUZZ_CASES=10000
 
 
 def _cases():
