@@ -80,3 +80,62 @@ def test_random_case(case):
     for j, (t, _) in enumerate(holders):  # inputs other than the in-place accumulator are untouched
         if not (inplace and j == 0):
             assert_same(from_dev(t, ins[j], offs[j]), ins[j], dt, f"input {j} modified")
+
+
+def _sync_cases():
+    rng = np.random.default_rng(777)
+    sizes = [0, 1, 17, 4096, 100_003, 300_007, 2_000_003, 9_000_001]
+    weights = np.array([1, 2, 2, 3, 3, 2, 1, 0.3])
+    out = []
+    for i in range(N_CASES // 4):
+        dt = int(rng.choice(ALL_DTYPES))
+        op = int(rng.choice(OPS))
+        k = int(rng.integers(1, 17))
+        n = int(rng.choice(sizes, p=weights / weights.sum()))
+        kinds = [int(x) for x in rng.integers(0, 3, size=k + 1)]  # 0 device, 1 pinned, 2 pageable
+        offs = [int(x) for x in rng.integers(0, 16, size=k + 1)]
+        inplace = bool(rng.random() < 0.5)
+        out.append((i, dt, op, k, n, kinds, offs, inplace))
+    return out
+
+
+SYNC_CASES = _sync_cases()
+
+
+@pytest.mark.parametrize("case", SYNC_CASES, ids=[f"s{c[0]}-{DT_NAME[c[1]]}-{OP_NAME[c[2]]}-k{c[3]}-n{c[4]}"
+                                                   for c in SYNC_CASES])
+def test_random_sync_case(case):
+    """The synchronous entry with a random pointer kind per operand (device,
+    pinned, pageable) at random element offsets: zero-copy, bounce buffers,
+    the staged pipeline with its drain thread, and their mixes."""
+    import torch
+    i, dt, op, k, n, kinds, offs, inplace = case
+    ins = [rand_array(dt, n, seed=50_000 + 97 * i + j, op=op) for j in range(k)]
+    flags = F_MINMAX_INOUT_FIRST if dt == FP16 else (bf16_flags(2) if dt == BF16 else 0)
+    exp = oracle.fanin(ins, dt, op, oracle.BF16_AVX512BF, oracle.FP16_AVX512F)
+    es = ins[0].itemsize
+    keep = []
+
+    def place(x, kind, off):
+        raw = np.zeros(x.size + off + 16, x.dtype)
+        raw[off:off + x.size] = x
+        if kind == 0:
+            t, p = to_dev(x, pad_elems=16, offset_elems=off)
+            keep.append(t)
+            return p, (lambda: from_dev(t, x, off))
+        if kind == 1:
+            h = torch.from_numpy(raw.view(np.uint8).copy()).pin_memory()
+            keep.append(h)
+            return h.data_ptr() + off * es, (lambda: h.numpy().view(x.dtype)[off:off + x.size].copy())
+        keep.append(raw)
+        return raw.ctypes.data + off * es, (lambda: raw[off:off + x.size].copy())
+
+    placed = [place(x, kinds[j], offs[j]) for j, x in enumerate(ins)]
+    if inplace:
+        po, read = placed[0]
+    else:
+        po, read = place(np.zeros_like(ins[0]), kinds[k], offs[k])
+    arr = _lib.void_ptr_array([p for p, _ in placed])
+    _lib.check(_lib.mi().mi_reduce_multi_sync(arr, k, po, n, dt, op, flags, -1))
+    if n:
+        assert_same(read(), exp, dt, f"case {case}")
