@@ -112,6 +112,35 @@ __global__ __launch_bounds__(B) void im_kernel(RKArgs a, float* sink) {
     }
 }
 
+// Persistent, software-pipelined fan-in: block b walks tiles b, b+G, ...;
+// tile t+G's K loads are issued BEFORE tile t's result is stored, so the
+// write of one tile overlaps the reads of the next instead of following
+// its own reads.  (pipe mode)
+template <int K, int B>
+__global__ __launch_bounds__(B) void pipe_kernel(RKArgs a) {
+    const uint64_t ntiles = a.nvec / B;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; j++)
+        x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in[j]) + t * B + threadIdx.x);
+    for (;;) {
+        f32x4 acc = __builtin_bit_cast(f32x4, x[0]);
+#pragma unroll
+        for (int j = 1; j < K; j++) acc = acc + __builtin_bit_cast(f32x4, x[j]);
+        const uint64_t tn = t + gridDim.x;
+        if (tn < ntiles) {
+#pragma unroll
+            for (int j = 0; j < K; j++)
+                x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in[j]) + tn * B + threadIdx.x);
+        }
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, acc), reinterpret_cast<u32x4*>(a.out) + t * B + threadIdx.x);
+        if (tn >= ntiles) break;
+        t = tn;
+    }
+}
+
 struct Variant {
     std::string name;
     double traffic;  // bytes per launch
@@ -257,11 +286,21 @@ void layouts(std::vector<Variant>& vs, size_t bytes, float* sink) {
     add_r2(vs, big8, big8 + bytes, big8 + 2 * bytes, nvec, b, "one allocation, out of place slots 0,1 -> 2");
 }
 
+template <int K, int B>
+void add_pipe(std::vector<Variant>& vs, const RKArgs& r, unsigned grid, double bytes) {
+    char name[128];
+    snprintf(name, sizeof name, "pipe persistent K=%d B=%d grid=%u", K, B, grid);
+    vs.push_back({name, (K + 1) * bytes, [r, grid](hipStream_t s) {
+                      hipLaunchKernelGGL((pipe_kernel<K, B>), dim3(grid), dim3(B), 0, s, r);
+                  }, {}});
+}
+
 int main(int argc, char** argv) {
     const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
     const int reps = argc > 3 ? atoi(argv[3]) : 8;
     const bool layout_mode = argc > 4 && std::string(argv[4]) == "layout";
+    const bool pipe_mode = argc > 4 && std::string(argv[4]) == "pipe";
     const size_t bytes = mib << 20;
     const uint64_t nvec = bytes / 16;
     std::vector<Variant> vs;
@@ -292,6 +331,24 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 8; i++) rc.in[i] = reinterpret_cast<char*>(big) + i * bytes;
     const double b = (double)bytes;
 
+    if (pipe_mode) {
+        add_fan(vs, r, 8, b, "");
+        for (unsigned g : {256u, 512u, 1024u, 2048u}) add_pipe<8, 1024>(vs, r, g, b);
+        for (unsigned g : {512u, 1024u, 2048u, 4096u}) add_pipe<8, 256>(vs, r, g, b);
+        add_readk<8>(vs, r, out, b, "");
+        // correctness (all inputs equal bytes -> 8 * x)
+        std::vector<float> h(4096), x(4096);
+        CK(hipMemcpy(x.data(), sep[0], 4096 * 4, hipMemcpyDeviceToHost));
+        hipLaunchKernelGGL((pipe_kernel<8, 1024>), dim3(512), dim3(1024), 0, s, r);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(h.data(), out, 4096 * 4, hipMemcpyDeviceToHost));
+        float e = x[0];
+        for (int i = 1; i < 8; i++) e = e + x[0];
+        int bad = 0;
+        for (int i = 0; i < 4096; i++) bad += (h[i] != e);
+        fprintf(stderr, "pipe fan check: %d mismatches\n", bad);
+        return run(vs, s, rounds, reps, mib);
+    }
     add_readk<8>(vs, r, out, b, "");
     add_readk<2>(vs, r, out, b, "");
     add_readk<8>(vs, rc, out, b, " contiguous-alloc");
