@@ -88,6 +88,7 @@ enum mi_dtype {
 #define MI_E_INVALID (-1)      /* bad dtype / op / k / NULL pointer      */
 #define MI_E_UNSUPPORTED (-2)  /* combination not implemented            */
 #define MI_E_NO_DEVICE (-3)    /* no HIP device visible                   */
+#define MI_E_RESOURCE (-4)     /* host resources (thread, memory) failed  */
 
 #define MI_MAX_INPUTS 16 /* the reference's monolithic fan-in covers 16 ranks
                             (src/kernels/kernels.cl:268)                   */

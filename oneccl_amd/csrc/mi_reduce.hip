@@ -891,6 +891,19 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
 
 }  // namespace
 
+// Host-side failures (a thread, allocation or lock that cannot be had) are
+// C++ exceptions; none may cross the C ABI.  They become MI_E_RESOURCE.
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        return fail(MI_E_RESOURCE, e.what());
+    } catch (...) {
+        return fail(MI_E_RESOURCE, "unexpected host-side exception");
+    }
+}
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -916,14 +929,18 @@ int mi_reduce_multi(const void* const* inputs, int k, void* out, size_t count, i
 
 int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,
                    int device) {
-    const void* ins[2] = {inout, in};
-    return reduce_sync(ins, 2, inout, count, dtype, op, flags, device);
+    return guarded([&]() -> int {
+        const void* ins[2] = {inout, in};
+        return reduce_sync(ins, 2, inout, count, dtype, op, flags, device);
+    });
 }
 
 int mi_reduce_multi_sync(const void* const* inputs, int k, void* out, size_t count, int dtype,
                          int op, unsigned flags, int device) {
-    if (!inputs) return fail(MI_E_INVALID, "null input list");
-    return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+    return guarded([&]() -> int {
+        if (!inputs) return fail(MI_E_INVALID, "null input list");
+        return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+    });
 }
 
 int mi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags,
@@ -933,59 +950,61 @@ int mi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t 
 
 int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags,
                     int device) {
-    if (!pick_conv(src_dtype, dst_dtype, flags))
-        return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
-    if (count == 0) return 0;
-    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
-    int pdev = -1;
-    const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
-    if (device < 0 && pdev >= 0) device = pdev;
-    DevCtx* d = nullptr;
-    int rc = get_ctx(device, &d);
-    if (rc) return rc;
-    int prev = 0;
-    MI_HIP(hipGetDevice(&prev));
-    if (prev != d->device) MI_HIP(hipSetDevice(d->device));
-    struct Restore {
-        int dev, cur;
-        ~Restore() {
-            if (dev != cur) (void)hipSetDevice(dev);
-        }
-    } restore{prev, d->device};
-    const uint64_t trunc_from = (count / 16) * 16;
-    if (ks == PK_DEVICE && kd == PK_DEVICE) {
-        rc = launch_convert(src, src_dtype, dst, dst_dtype, count, flags, d->stream[0], trunc_from);
+    return guarded([&]() -> int {
+        if (!pick_conv(src_dtype, dst_dtype, flags))
+            return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
+        if (count == 0) return 0;
+        if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+        int pdev = -1;
+        const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+        if (device < 0 && pdev >= 0) device = pdev;
+        DevCtx* d = nullptr;
+        int rc = get_ctx(device, &d);
         if (rc) return rc;
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+        struct Restore {
+            int dev, cur;
+            ~Restore() {
+                if (dev != cur) (void)hipSetDevice(dev);
+            }
+        } restore{prev, d->device};
+        const uint64_t trunc_from = (count / 16) * 16;
+        if (ks == PK_DEVICE && kd == PK_DEVICE) {
+            rc = launch_convert(src, src_dtype, dst, dst_dtype, count, flags, d->stream[0], trunc_from);
+            if (rc) return rc;
+            MI_HIP(wait_stream(d->stream[0]));
+            return 0;
+        }
+        const size_t ss = dtype_size(src_dtype), ds = dtype_size(dst_dtype);
+        size_t chunk = kChunkBytes / std::max(ss, ds);
+        chunk -= chunk % 16;
+        rc = ensure_scratch(d, 2, chunk * std::max(ss, ds));
+        if (rc) return rc;
+        for (size_t off = 0, c = 0; off < count; off += chunk, c++) {
+            const int sl = (int)(c & 1);
+            hipStream_t st = d->stream[sl];
+            const size_t n = std::min(chunk, count - off);
+            const void* sp = static_cast<const char*>(src) + off * ss;
+            void* dp = static_cast<char*>(dst) + off * ds;
+            const void* dsrc = sp;
+            void* ddst = dp;
+            if (ks != PK_DEVICE) {
+                MI_HIP(hipMemcpyAsync(d->dbuf[sl][0], sp, n * ss, hipMemcpyHostToDevice, st));
+                dsrc = d->dbuf[sl][0];
+            }
+            if (kd != PK_DEVICE) ddst = d->dbuf[sl][1];
+            // chunk starts are multiples of 16: the tail split is the global one
+            rc = launch_convert(dsrc, src_dtype, ddst, dst_dtype, n, flags, st,
+                                trunc_from > off ? std::min<uint64_t>(trunc_from - off, n) : 0);
+            if (rc) return rc;
+            if (kd != PK_DEVICE) MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
+        }
         MI_HIP(wait_stream(d->stream[0]));
+        MI_HIP(wait_stream(d->stream[1]));
         return 0;
-    }
-    const size_t ss = dtype_size(src_dtype), ds = dtype_size(dst_dtype);
-    size_t chunk = kChunkBytes / std::max(ss, ds);
-    chunk -= chunk % 16;
-    rc = ensure_scratch(d, 2, chunk * std::max(ss, ds));
-    if (rc) return rc;
-    for (size_t off = 0, c = 0; off < count; off += chunk, c++) {
-        const int sl = (int)(c & 1);
-        hipStream_t st = d->stream[sl];
-        const size_t n = std::min(chunk, count - off);
-        const void* sp = static_cast<const char*>(src) + off * ss;
-        void* dp = static_cast<char*>(dst) + off * ds;
-        const void* dsrc = sp;
-        void* ddst = dp;
-        if (ks != PK_DEVICE) {
-            MI_HIP(hipMemcpyAsync(d->dbuf[sl][0], sp, n * ss, hipMemcpyHostToDevice, st));
-            dsrc = d->dbuf[sl][0];
-        }
-        if (kd != PK_DEVICE) ddst = d->dbuf[sl][1];
-        // chunk starts are multiples of 16: the tail split is the global one
-        rc = launch_convert(dsrc, src_dtype, ddst, dst_dtype, n, flags, st,
-                            trunc_from > off ? std::min<uint64_t>(trunc_from - off, n) : 0);
-        if (rc) return rc;
-        if (kd != PK_DEVICE) MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
-    }
-    MI_HIP(wait_stream(d->stream[0]));
-    MI_HIP(wait_stream(d->stream[1]));
-    return 0;
+    });
 }
 
 // ---- asynchronous requests ------------------------------------------------
@@ -998,59 +1017,61 @@ struct mi_request {
 
 int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
                     unsigned flags, int device, mi_request_t* req) {
-    if (!req) return fail(MI_E_INVALID, "null request pointer");
-    *req = nullptr;
-    if (!inputs) return fail(MI_E_INVALID, "null input list");
-    if (!dtype_size(dtype)) return fail(MI_E_INVALID, "unknown datatype");
-    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
-    if (count > 0) {
-        if (!out) return fail(MI_E_INVALID, "null output");
-        for (int i = 0; i < k; i++)
-            if (!inputs[i]) return fail(MI_E_INVALID, "null input");
-        if (op < MI_OP_SUM || op > MI_OP_MAX)
-            return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
-        if (needs_staging(inputs, k, out)) {
-            auto j = std::make_shared<AsyncJob>();
-            for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
-            j->k = k;
-            j->out = out;
-            j->count = count;
-            j->dt = dtype;
-            j->op = op;
-            j->flags = flags;
-            j->device = device;
-            t_stage.submit(j);
-            mi_request* r = new mi_request();
-            r->job = j;
-            *req = r;
-            return 0;
+    return guarded([&]() -> int {
+        if (!req) return fail(MI_E_INVALID, "null request pointer");
+        *req = nullptr;
+        if (!inputs) return fail(MI_E_INVALID, "null input list");
+        if (!dtype_size(dtype)) return fail(MI_E_INVALID, "unknown datatype");
+        if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+        if (count > 0) {
+            if (!out) return fail(MI_E_INVALID, "null output");
+            for (int i = 0; i < k; i++)
+                if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+            if (op < MI_OP_SUM || op > MI_OP_MAX)
+                return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
+            if (needs_staging(inputs, k, out)) {
+                auto j = std::make_shared<AsyncJob>();
+                for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
+                j->k = k;
+                j->out = out;
+                j->count = count;
+                j->dt = dtype;
+                j->op = op;
+                j->flags = flags;
+                j->device = device;
+                t_stage.submit(j);
+                mi_request* r = new mi_request();
+                r->job = j;
+                *req = r;
+                return 0;
+            }
         }
-    }
-    DevCtx* d = nullptr;
-    int used = 0;
-    int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used);
-    if (rc) return rc;
-    mi_request* r = new mi_request();
-    if (d) {
-        r->device = d->device;
-        int prev = 0;
-        MI_HIP(hipGetDevice(&prev));
-        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
-        for (int s = 0; s < 2 && rc == 0; s++) {
-            if (!(used & (1 << s))) continue;
-            hipError_t e = hipEventCreateWithFlags(&r->ev[r->nev], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventRecord(r->ev[r->nev], d->stream[s]);
-            if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
-            r->nev++;
+        DevCtx* d = nullptr;
+        int used = 0;
+        int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used);
+        if (rc) return rc;
+        mi_request* r = new mi_request();
+        if (d) {
+            r->device = d->device;
+            int prev = 0;
+            MI_HIP(hipGetDevice(&prev));
+            if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+            for (int s = 0; s < 2 && rc == 0; s++) {
+                if (!(used & (1 << s))) continue;
+                hipError_t e = hipEventCreateWithFlags(&r->ev[r->nev], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventRecord(r->ev[r->nev], d->stream[s]);
+                if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+                r->nev++;
+            }
+            if (prev != d->device) (void)hipSetDevice(prev);
         }
-        if (prev != d->device) (void)hipSetDevice(prev);
-    }
-    if (rc) {
-        mi_request_free(r);
-        return rc;
-    }
-    *req = r;
-    return 0;
+        if (rc) {
+            mi_request_free(r);
+            return rc;
+        }
+        *req = r;
+        return 0;
+    });
 }
 
 int mi_test(mi_request_t req, int* done) {
@@ -1096,75 +1117,79 @@ int mi_request_free(mi_request_t req) {
 // ---- one bucket split over several GPUs, any pointer kinds -----------------
 int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
                                  unsigned flags, int nshards, const int* devices) {
-    if (!inputs || !devices || nshards < 1) return fail(MI_E_INVALID, "bad shard arguments");
-    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
-    const size_t es = dtype_size(dtype);
-    if (!es) return fail(MI_E_INVALID, "unknown datatype");
-    if (nshards == 1 || count == 0) return reduce_sync(inputs, k, out, count, dtype, op, flags, devices[0]);
-    // Shards start on 256-element boundaries, so the bf16 count % 16 tail
-    // (MI_F_BF16_TAIL_TRUNC16) lies in the last shard exactly as in the
-    // whole array.  Shard 0 runs on the calling thread, the others on
-    // workers owned by it (one per shard slot, persistent streams/staging).
-    thread_local std::vector<std::unique_ptr<StageWorker>> t_shard_workers;
-    while ((int)t_shard_workers.size() < nshards - 1) t_shard_workers.emplace_back(new StageWorker());
-    const size_t per = ((count + (size_t)nshards - 1) / (size_t)nshards + 255) / 256 * 256;
-    std::vector<std::shared_ptr<AsyncJob>> jobs;
-    for (int sh = 1; sh < nshards; sh++) {
-        const size_t b = std::min(count, per * (size_t)sh), e = std::min(count, b + per);
-        if (b >= e) break;
-        auto j = std::make_shared<AsyncJob>();
-        for (int i = 0; i < k; i++) j->inputs[i] = static_cast<const char*>(inputs[i]) + b * es;
-        j->k = k;
-        j->out = static_cast<char*>(out) + b * es;
-        j->count = e - b;
-        j->dt = dtype;
-        j->op = op;
-        j->flags = flags;
-        j->device = devices[sh];
-        t_shard_workers[sh - 1]->submit(j);
-        jobs.push_back(j);
-    }
-    const int rc0 = reduce_sync(inputs, k, out, std::min(count, per), dtype, op, flags, devices[0]);
-    std::string err0 = rc0 ? g_last_error : std::string();
-    int rc = rc0;
-    for (auto& j : jobs) {
-        const int r = j->wait();  // every shard finishes before the call returns
-        if (r && !rc) {
-            rc = r;
-            err0 = j->err;
+    return guarded([&]() -> int {
+        if (!inputs || !devices || nshards < 1) return fail(MI_E_INVALID, "bad shard arguments");
+        if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+        const size_t es = dtype_size(dtype);
+        if (!es) return fail(MI_E_INVALID, "unknown datatype");
+        if (nshards == 1 || count == 0) return reduce_sync(inputs, k, out, count, dtype, op, flags, devices[0]);
+        // Shards start on 256-element boundaries, so the bf16 count % 16 tail
+        // (MI_F_BF16_TAIL_TRUNC16) lies in the last shard exactly as in the
+        // whole array.  Shard 0 runs on the calling thread, the others on
+        // workers owned by it (one per shard slot, persistent streams/staging).
+        thread_local std::vector<std::unique_ptr<StageWorker>> t_shard_workers;
+        while ((int)t_shard_workers.size() < nshards - 1) t_shard_workers.emplace_back(new StageWorker());
+        const size_t per = ((count + (size_t)nshards - 1) / (size_t)nshards + 255) / 256 * 256;
+        std::vector<std::shared_ptr<AsyncJob>> jobs;
+        for (int sh = 1; sh < nshards; sh++) {
+            const size_t b = std::min(count, per * (size_t)sh), e = std::min(count, b + per);
+            if (b >= e) break;
+            auto j = std::make_shared<AsyncJob>();
+            for (int i = 0; i < k; i++) j->inputs[i] = static_cast<const char*>(inputs[i]) + b * es;
+            j->k = k;
+            j->out = static_cast<char*>(out) + b * es;
+            j->count = e - b;
+            j->dt = dtype;
+            j->op = op;
+            j->flags = flags;
+            j->device = devices[sh];
+            t_shard_workers[sh - 1]->submit(j);
+            jobs.push_back(j);
         }
-    }
-    return rc ? fail(rc, err0.c_str()) : 0;
+        const int rc0 = reduce_sync(inputs, k, out, std::min(count, per), dtype, op, flags, devices[0]);
+        std::string err0 = rc0 ? g_last_error : std::string();
+        int rc = rc0;
+        for (auto& j : jobs) {
+            const int r = j->wait();  // every shard finishes before the call returns
+            if (r && !rc) {
+                rc = r;
+                err0 = j->err;
+            }
+        }
+        return rc ? fail(rc, err0.c_str()) : 0;
+    });
 }
 
 // ---- in-process multi-GPU element-range shards -------------------------------
 int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs, int k, void* const* outs,
                       const size_t* counts, int dtype, int op, unsigned flags) {
-    if (nshards < 1 || !devices || !inputs || !outs || !counts) return fail(MI_E_INVALID, "bad shard arguments");
-    if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
-    int prev = 0;
-    MI_HIP(hipGetDevice(&prev));
-    std::vector<DevCtx*> ctx((size_t)nshards, nullptr);
-    int rc = 0;
-    // launch every shard before waiting for any
-    for (int s = 0; s < nshards && rc == 0; s++) {
-        rc = get_ctx(devices[s], &ctx[s]);
-        if (rc) break;
-        hipError_t e = hipSetDevice(devices[s]);
-        if (e != hipSuccess) {
-            rc = hip_fail(e, "hipSetDevice");
-            break;
+    return guarded([&]() -> int {
+        if (nshards < 1 || !devices || !inputs || !outs || !counts) return fail(MI_E_INVALID, "bad shard arguments");
+        if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        std::vector<DevCtx*> ctx((size_t)nshards, nullptr);
+        int rc = 0;
+        // launch every shard before waiting for any
+        for (int s = 0; s < nshards && rc == 0; s++) {
+            rc = get_ctx(devices[s], &ctx[s]);
+            if (rc) break;
+            hipError_t e = hipSetDevice(devices[s]);
+            if (e != hipSuccess) {
+                rc = hip_fail(e, "hipSetDevice");
+                break;
+            }
+            rc = launch_reduce(inputs + (size_t)s * k, k, outs[s], counts[s], dtype, op, flags, ctx[s]->stream[0]);
         }
-        rc = launch_reduce(inputs + (size_t)s * k, k, outs[s], counts[s], dtype, op, flags, ctx[s]->stream[0]);
-    }
-    for (int s = 0; s < nshards; s++) {
-        if (!ctx[s]) continue;
-        (void)hipSetDevice(devices[s]);
-        const hipError_t e = wait_stream(ctx[s]->stream[0]);
-        if (e != hipSuccess && rc == 0) rc = hip_fail(e, "hipStreamSynchronize");
-    }
-    (void)hipSetDevice(prev);
-    return rc;
+        for (int s = 0; s < nshards; s++) {
+            if (!ctx[s]) continue;
+            (void)hipSetDevice(devices[s]);
+            const hipError_t e = wait_stream(ctx[s]->stream[0]);
+            if (e != hipSuccess && rc == 0) rc = hip_fail(e, "hipStreamSynchronize");
+        }
+        (void)hipSetDevice(prev);
+        return rc;
+    });
 }
 
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {
@@ -1193,29 +1218,31 @@ int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* str
 }
 
 int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int device) {
-    if (bytes == 0) return 0;
-    if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
-    int pdev = -1;
-    const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
-    if (device < 0 && pdev >= 0) device = pdev;
-    DevCtx* d = nullptr;
-    int rc = get_ctx(device, &d);
-    if (rc) return rc;
-    if (ks == PK_DEVICE && kd == PK_DEVICE) {
-        int prev = 0;
-        MI_HIP(hipGetDevice(&prev));
-        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
-        rc = mi_copy(src, dst, bytes, nontemporal, d->stream[0]);
-        if (!rc) {
-            hipError_t e = wait_stream(d->stream[0]);
-            if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    return guarded([&]() -> int {
+        if (bytes == 0) return 0;
+        if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
+        int pdev = -1;
+        const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+        if (device < 0 && pdev >= 0) device = pdev;
+        DevCtx* d = nullptr;
+        int rc = get_ctx(device, &d);
+        if (rc) return rc;
+        if (ks == PK_DEVICE && kd == PK_DEVICE) {
+            int prev = 0;
+            MI_HIP(hipGetDevice(&prev));
+            if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+            rc = mi_copy(src, dst, bytes, nontemporal, d->stream[0]);
+            if (!rc) {
+                hipError_t e = wait_stream(d->stream[0]);
+                if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+            }
+            if (prev != d->device) (void)hipSetDevice(prev);
+            return rc;
         }
-        if (prev != d->device) (void)hipSetDevice(prev);
-        return rc;
-    }
-    MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
-    MI_HIP(wait_stream(d->stream[0]));
-    return 0;
+        MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
+        MI_HIP(wait_stream(d->stream[0]));
+        return 0;
+    });
 }
 
 int mi_shard_range(size_t count, int rank, int world, size_t align, size_t* begin, size_t* end) {
