@@ -85,7 +85,23 @@ int main(int argc, char** argv) {
     });
     measure("mi_reduce_sync 4 KiB device", reps, [&] { mi_reduce_sync(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
     measure("mi_reduce_sync 4 KiB pinned host (zero-copy)", reps, [&] { mi_reduce_sync(ha, hb, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
-    measure("mi_reduce_sync 4 KiB pageable host (staged)", reps / 4,
+    {
+        const void* ins[2] = {b, a};
+        measure("mi_reduce_start + mi_wait + mi_request_free 4 KiB device", reps, [&] {
+            mi_request_t r = nullptr;
+            mi_reduce_start(ins, 2, b, n, MI_FLOAT32, MI_OP_SUM, 0, -1, &r);
+            mi_wait(r);
+            mi_request_free(r);
+        });
+        measure("mi_reduce_start + mi_request_free 4 KiB device (host side; a device request's free does not wait)",
+                reps / 4, [&] {
+                    mi_request_t r = nullptr;
+                    mi_reduce_start(ins, 2, b, n, MI_FLOAT32, MI_OP_SUM, 0, -1, &r);
+                    mi_request_free(r);
+                });
+        (void)hipDeviceSynchronize();
+    }
+    measure("mi_reduce_sync 4 KiB pageable host (bounce)", reps / 4,
             [&] { mi_reduce_sync(pa.data(), pb.data(), n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
     return 0;
 }
