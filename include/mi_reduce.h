@@ -117,6 +117,26 @@ int mi_reduce_out(const void* in1, const void* in2, void* out, size_t count,
 int mi_reduce_multi(const void* const* inputs, int k, void* out, size_t count,
                     int dtype, int op, unsigned flags, void* stream);
 
+/* n independent mi_reduce calls in one dispatch: descs[i].inout =
+ * op(descs[i].in, descs[i].inout) over descs[i].count elements, all with one
+ * dtype / op / flags.  Results are those of the n mi_reduce calls in any
+ * order.  So no descriptor's inout may overlap another descriptor's in or
+ * inout (MI_E_INVALID); in == inout within one descriptor is allowed, as for
+ * mi_reduce.  For schedule phases with many small chunks: a sub-MiB reduce
+ * costs one dispatch, and this pays one for up to 64 chunks.
+ * No reference counterpart: oneCCL issues one ccl_comp_reduce per entry
+ * (reduce_local_entry.cpp:98-114, and one per parallelizer part,
+ * parallelizer.cpp:184-320).  An extension for callers that hold several
+ * chunks of one phase.                                                      */
+typedef struct mi_reduce_desc {
+    const void* in;
+    void* inout;
+    size_t count;
+} mi_reduce_desc_t;
+
+int mi_reduce_batch(const mi_reduce_desc_t* descs, int n, int dtype, int op,
+                    unsigned flags, void* stream);
+
 /* ---- synchronous, pointer-kind-agnostic entry (what src/comp calls) --- *
  * Same math as mi_reduce, but `in`/`inout` may each be device memory,
  * pinned host memory or pageable host memory; returns only when the result

@@ -30,11 +30,17 @@ def _load(name: str) -> ctypes.CDLL:
     return ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
 
 
+class MiReduceDesc(ctypes.Structure):
+    """mi_reduce_desc_t (include/mi_reduce.h)."""
+    _fields_ = [("in_", c_void_p), ("inout", c_void_p), ("count", c_size_t)]
+
+
 # (name, restype, argtypes) — mirrors include/mi_reduce.h
 MI_API = [
     ("mi_reduce", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_uint, c_void_p]),
     ("mi_reduce_out", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_uint, c_void_p]),
     ("mi_reduce_multi", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_void_p]),
+    ("mi_reduce_batch", c_int, [POINTER(MiReduceDesc), c_int, c_int, c_int, c_uint, c_void_p]),
     ("mi_reduce_sync", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_uint, c_int]),
     ("mi_reduce_multi_sync", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int]),
     ("mi_convert", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_void_p]),
@@ -133,6 +139,14 @@ def void_ptr_array(ptrs) -> ctypes.Array:
     arr = (c_void_p * len(ptrs))()
     for i, p in enumerate(ptrs):
         arr[i] = p
+    return arr
+
+
+def desc_array(triples) -> ctypes.Array:
+    """[(in_ptr, inout_ptr, count), ...] -> mi_reduce_desc_t[]."""
+    arr = (MiReduceDesc * max(len(triples), 1))()
+    for i, (a, b, n) in enumerate(triples):
+        arr[i] = MiReduceDesc(a, b, n)
     return arr
 
 

@@ -147,6 +147,7 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
 // ---------------------------------------------------------------------------
 typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
 typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
+typedef hipError_t (*LaunchBFn)(dim3, hipStream_t, const BArgs&);
 
 // Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
 constexpr int kB2 = 1024;
@@ -172,6 +173,12 @@ hipError_t launch_lean(dim3 grid, hipStream_t s, const R2Args& a) {
 }
 
 template <typename Tag, int OP, unsigned V>
+hipError_t launch_batch(dim3 grid, hipStream_t s, const BArgs& a) {
+    hipLaunchKernelGGL((reduce2_batch_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename Tag, int OP, unsigned V>
 hipError_t launch_fan(dim3, hipStream_t s, const KArgs& a) {
     constexpr int B = fan_block<Tag>();
     const uint64_t blocks = std::max<uint64_t>((a.nvec + B - 1) / B, 1);
@@ -190,6 +197,7 @@ struct Kern {
     LaunchFn general = nullptr;
     Launch2Fn lean = nullptr;
     LaunchFn fan = nullptr;
+    LaunchBFn batch = nullptr;
 };
 
 template <typename Tag, int OP, unsigned V>
@@ -210,6 +218,7 @@ Kern entry() {
         k.general = &launch_general<Tag, OP, V>;
         k.lean = &launch_lean<Tag, OP, V>;
         k.fan = &launch_fan<Tag, OP, V>;
+        k.batch = &launch_batch<Tag, OP, V>;
     }
     return k;
 }
@@ -390,6 +399,103 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
     }
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// descriptor batch: independent 2-input reduces in one launch
+// ---------------------------------------------------------------------------
+// Outputs must be pairwise disjoint and disjoint from other descriptors'
+// inputs, or the result would depend on which tile ran first.
+int check_batch_disjoint(const mi_reduce_desc_t* d, int n, size_t es) {
+    struct Rng {
+        uintptr_t lo, hi;
+        int owner;
+    };
+    std::vector<Rng> outs;
+    outs.reserve(n);
+    for (int i = 0; i < n; i++)
+        if (d[i].count) {
+            const uintptr_t lo = reinterpret_cast<uintptr_t>(d[i].inout);
+            outs.push_back({lo, lo + d[i].count * es, i});
+        }
+    std::sort(outs.begin(), outs.end(), [](const Rng& x, const Rng& y) { return x.lo < y.lo; });
+    for (size_t j = 1; j < outs.size(); j++)
+        if (outs[j].lo < outs[j - 1].hi) return fail(MI_E_INVALID, "batch descriptors' outputs overlap");
+    // outs are disjoint and sorted, so their ends are sorted too
+    for (int i = 0; i < n; i++) {
+        if (!d[i].count) continue;
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(d[i].in), hi = lo + d[i].count * es;
+        auto it = std::upper_bound(outs.begin(), outs.end(), lo,
+                                   [](uintptr_t v, const Rng& r) { return v < r.hi; });
+        for (; it != outs.end() && it->lo < hi; ++it)
+            if (it->owner != i) return fail(MI_E_INVALID, "a batch input overlaps another descriptor's output");
+    }
+    return 0;
+}
+
+int launch_reduce_batch(const mi_reduce_desc_t* d, int n, int dt, int op, unsigned flags,
+                        hipStream_t stream) {
+    const size_t es = dtype_size(dt);
+    if (!es) return fail(MI_E_INVALID, "unknown datatype");
+    if (op < MI_OP_SUM || op > MI_OP_MAX) return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
+    if (n < 0) return fail(MI_E_INVALID, "negative descriptor count");
+    if (n == 0) return 0;
+    if (!d) return fail(MI_E_INVALID, "null descriptor list");
+    for (int i = 0; i < n; i++) {
+        if (!d[i].count) continue;
+        if (!d[i].in || !d[i].inout) return fail(MI_E_INVALID, "null operand in batch descriptor");
+        if (int rc = require_gpu_visible(d[i].in)) return rc;
+        if (int rc = require_gpu_visible(d[i].inout)) return rc;
+    }
+    if (int rc = check_batch_disjoint(d, n, es)) return rc;
+    const unsigned v = canon_flags(dt, op, flags, 2);
+    const Kern kern = pick(dt, op, v);
+    if (!kern.batch) return fail(MI_E_UNSUPPORTED, "no kernel for this dtype/op/variant");
+
+    const uint64_t tile = (uint64_t)kB2 * kU2;
+    const size_t n_per_vec = 16 / es;
+    BArgs a;
+    memset(&a, 0, sizeof(a));
+    uint64_t blocks = 0;
+    auto flush = [&]() -> int {
+        if (!a.n) return 0;
+        a.block0[a.n] = (uint32_t)blocks;
+        const hipError_t e = kern.batch(dim3((unsigned)blocks), stream, a);
+        if (e != hipSuccess) return hip_fail(e, "kernel launch");
+        memset(&a, 0, sizeof(a));
+        blocks = 0;
+        return 0;
+    };
+    for (int i = 0; i < n; i++) {
+        const size_t count = d[i].count;
+        if (!count) continue;
+        // the same vector-grid decision as launch_reduce for k = 2
+        const uintptr_t mis = reinterpret_cast<uintptr_t>(d[i].inout) & 15u;
+        const uintptr_t pin = reinterpret_cast<uintptr_t>(d[i].in);
+        const bool elem = (mis % es) == 0 && (pin % es) == 0;
+        const bool vec = (elem && (pin & 15u) == mis) || (elem && unaligned_vectors());
+        const uint64_t head = vec && mis ? std::min<size_t>((16 - mis) / es, count) : 0;
+        const uint64_t nvec = vec ? (count - head) / n_per_vec : 0;
+        const uint64_t nb = std::max<uint64_t>((nvec + tile - 1) / tile, 1);
+        if (!vec || max_blocks() != 0 || nb > 0x40000000ull) {  // element loop / grid knob / huge: own launch
+            const void* ins[2] = {d[i].inout, d[i].in};
+            if (int rc = launch_reduce(ins, 2, d[i].inout, count, dt, op, flags, stream)) return rc;
+            continue;
+        }
+        if (a.n == kBatchMax || blocks + nb > 0x7FFFFFFFull)
+            if (int rc = flush()) return rc;
+        const int j = a.n++;
+        a.acc[j] = d[i].inout;
+        a.in[j] = d[i].in;
+        a.out[j] = d[i].inout;
+        a.nvec[j] = nvec;
+        a.head[j] = (uint8_t)head;
+        a.tail[j] = (uint8_t)(count - head - nvec * n_per_vec);
+        a.trunc_from[j] = (count / 16) * 16;
+        a.block0[j] = (uint32_t)blocks;
+        blocks += nb;
+    }
+    return flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -925,6 +1031,11 @@ int mi_reduce_multi(const void* const* inputs, int k, void* out, size_t count, i
                     unsigned flags, void* stream) {
     if (!inputs) return fail(MI_E_INVALID, "null input list");
     return launch_reduce(inputs, k, out, count, dtype, op, flags, (hipStream_t)stream);
+}
+
+int mi_reduce_batch(const mi_reduce_desc_t* descs, int n, int dtype, int op, unsigned flags,
+                    void* stream) {
+    return guarded([&]() -> int { return launch_reduce_batch(descs, n, dtype, op, flags, (hipStream_t)stream); });
 }
 
 int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,

@@ -455,12 +455,14 @@ __device__ __forceinline__ void reduce2_elem(const R2Args& a, uint64_t idx) {
     static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
 }
 
+// One tile (block `blk` of the operand set `a`): the body of reduce2_kernel,
+// shared with the descriptor-batched form below.
 template <typename Tag, int OP, unsigned V, int U, int B>
-__global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
+__device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
     constexpr int N = 16 / sizeof(S);
-    if (blockIdx.x == 0) {
+    if (blk == 0) {
         if (threadIdx.x < a.head) reduce2_elem<Tag, OP, V>(a, threadIdx.x);
         if (threadIdx.x < a.tail) reduce2_elem<Tag, OP, V>(a, a.head + a.nvec * N + threadIdx.x);
     }
@@ -468,7 +470,7 @@ __global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
     const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.acc) + hb);
     const u32x4* p1 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in) + hb);
     u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
-    const uint64_t v0 = (uint64_t)blockIdx.x * (B * U) + threadIdx.x;
+    const uint64_t v0 = (uint64_t)blk * (B * U) + threadIdx.x;
     u32x4 x[U], y[U];
     const bool full = v0 + (uint64_t)(U - 1) * B < a.nvec;
 #pragma unroll
@@ -490,6 +492,52 @@ __global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
             vstore<3>(po + v, __builtin_bit_cast(u32x4, pr));
         }
     }
+}
+
+template <typename Tag, int OP, unsigned V, int U, int B>
+__global__ __launch_bounds__(B) void reduce2_kernel(R2Args a) {
+    reduce2_tile<Tag, OP, V, U, B>(a, blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// Descriptor-batched 2-input reduce: up to kBatchMax independent
+// (acc, in, out) operand sets in one launch, each cut into reduce2_kernel's
+// tiles.  Block b works on descriptor d = the last one with block0[d] <= b
+// (a uniform binary search over the kernarg table), tile b - block0[d].  For
+// schedules with many small chunks in one phase: one dispatch instead of one
+// per chunk (sub-MiB reduces are dispatch-bound).
+// ---------------------------------------------------------------------------
+constexpr int kBatchMax = 64;
+
+struct BArgs {
+    const void* acc[kBatchMax];
+    const void* in[kBatchMax];
+    void* out[kBatchMax];
+    uint64_t nvec[kBatchMax];
+    uint64_t trunc_from[kBatchMax];
+    uint8_t head[kBatchMax], tail[kBatchMax];  // < 16 elements each
+    uint32_t block0[kBatchMax + 1];             // first block of each descriptor; [n] = grid size
+    int n;
+};
+
+template <typename Tag, int OP, unsigned V, int U, int B>
+__global__ __launch_bounds__(B) void reduce2_batch_kernel(BArgs a) {
+    const uint32_t b = blockIdx.x;
+    int lo = 0, hi = a.n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.block0[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    R2Args r;
+    r.acc = a.acc[lo];
+    r.in = a.in[lo];
+    r.out = a.out[lo];
+    r.nvec = a.nvec[lo];
+    r.head = a.head[lo];
+    r.tail = a.tail[lo];
+    r.trunc_from = a.trunc_from[lo];
+    reduce2_tile<Tag, OP, V, U, B>(r, b - a.block0[lo]);
 }
 
 // ---------------------------------------------------------------------------

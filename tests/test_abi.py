@@ -110,6 +110,12 @@ def test_argument_errors_need_no_device():
     assert m.mi_reduce(0, 0, 10, 9, 4, 0, None) == -1  # custom is host-only
     arr = _lib.void_ptr_array([0] * 17)
     assert m.mi_reduce_multi(arr, 17, 0, 10, 9, 0, 0, None) == -1
+    assert m.mi_reduce_batch(None, 0, 9, 0, 0, None) == 0  # empty batch
+    assert m.mi_reduce_batch(None, 3, 9, 0, 0, None) == -1
+    assert m.mi_reduce_batch(_lib.desc_array([]), -1, 9, 0, 0, None) == -1
+    assert m.mi_reduce_batch(_lib.desc_array([(0, 0, 10)]), 1, 42, 0, 0, None) == -1
+    assert m.mi_reduce_batch(_lib.desc_array([(0, 0, 0), (0, 0, 0)]), 2, 9, 0, 0, None) == 0  # all empty
+    assert m.mi_reduce_batch(_lib.desc_array([(0, 0, 5)]), 1, 9, 0, 0, None) == -1  # null operand
 
 
 def test_device_entry_points_refuse_pageable_memory():
@@ -125,6 +131,7 @@ def test_device_entry_points_refuse_pageable_memory():
     assert m.mi_reduce_multi(_lib.void_ptr_array([pa, pb, pa]), 3, pb, 64, 9, 0, 0, None) == -1
     assert m.mi_convert(pa, 9, pb, 11, 64, 0, None) == -1
     assert m.mi_copy(pa, pb, 256, 0, None) == -1
+    assert m.mi_reduce_batch(_lib.desc_array([(pa, pb, 64)]), 1, 9, 0, 0, None) == -1
 
 
 @pytest.mark.parametrize("count", [0, 1, 255, 256, 1000, 1 << 28, (1 << 28) + 3])

@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Launch cost of a chain of small reduces: eager calls vs one captured HIP
-graph replay.  A oneCCL ring schedule issues one reduce per chunk per step;
+graph replay vs one mi_reduce_batch dispatch.  A oneCCL ring schedule issues one reduce per chunk per step;
 below ~1 MiB each call is bound by dispatch latency, so the
 question is what a replayed graph of the same chain costs per reduce.
 
 For each bucket size and chain length L: L in-place fp32 sum reduces
 (mi_reduce) on distinct chunk pairs, issued (a) eagerly on one stream, timed
 with events around the whole chain, (b) captured once into a torch CUDA graph
-and replayed.  Prints one JSON line per point.
+and replayed, (c) as one mi_reduce_batch call over the L descriptors.  Prints one JSON line per point.
 
   python tools/graph_probe.py [--reps 50] > out.jsonl
 """
@@ -66,10 +66,14 @@ def main() -> None:
             with torch.cuda.graph(g):
                 chain(torch.cuda.current_stream().cuda_stream)
             graph, graph_w = timed(g.replay)
+            descs = _lib.desc_array([(b.data_ptr(), a.data_ptr(), n) for a, b in zip(acc, inp)])
+            batch, batch_w = timed(lambda: _lib.check(
+                m.mi_reduce_batch(descs, L, FP32, SUM, 0, stream.cuda_stream), "mi_reduce_batch"))
             print(json.dumps({"bucket_bytes": nbytes, "chain": L, "eager_us": round(eager, 2),
                               "graph_us": round(graph, 2), "eager_us_per_reduce": round(eager / L, 2),
                               "graph_us_per_reduce": round(graph / L, 2),
                               "eager_wall_us": round(eager_w, 2), "graph_wall_us": round(graph_w, 2),
+                              "batch_us": round(batch, 2), "batch_wall_us": round(batch_w, 2),
                               "timing": "torch events on the issuing stream around the chain (gpu) and host clock from "
                                         "first call to completion (wall); median of "
                                         f"{args.reps}"}), flush=True)
