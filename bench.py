@@ -407,7 +407,7 @@ def pmc_traffic(config):
             d = json.loads(p.read_text())
         except (OSError, ValueError):
             continue
-        if config in d:
+        if isinstance(d.get(config), dict) and "hbm_bytes_per_launch" in d[config]:
             return {"bytes_per_launch": d[config]["hbm_bytes_per_launch"], "source": str(p.relative_to(ROOT))}
     return None
 
