@@ -38,6 +38,11 @@ int mi_ccl_comp_reduce_custom(const void* in_buf, size_t in_count, void* inout_b
 int mi_ccl_comp_batch_reduce(const void* in_buf, const size_t* offsets, size_t n_offsets,
                              size_t in_count, void* inout_buf, size_t* out_count, int dtype,
                              int op, int bf16_keep_precision_mode);
+/* ccl_comp_batch_reduce with reduction::custom and the user's callback
+ * (every input folded by fn, in keep-precision mode on the fp32 scratch). */
+int mi_ccl_comp_batch_reduce_custom(const void* in_buf, const size_t* offsets, size_t n_offsets,
+                                    size_t in_count, void* inout_buf, size_t* out_count, int dtype,
+                                    int bf16_keep_precision_mode, mi_ccl_reduction_fn fn);
 /* ccl_comp_copy, src/comp/comp.cpp:60-74 */
 int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal);
 /* ccl_bf16_reduce, src/comp/bf16/bf16.cpp:87-110 (MPI user-op entry,

@@ -144,25 +144,40 @@ def build_asan(force: bool = False) -> Path:
 
 
 def build_oracle(force: bool = False) -> Path:
-    """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile)."""
+    """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile), and, where the
+    reference tree is present (this container, not the GPU box), the harness
+    over the reference's own bf16/fp16 code (oracle/_ref, `make -C oracle ref`)."""
     odir = ROOT / "oracle"
     if force:
         _run(["make", "-C", str(odir), "clean"])
     _run(["make", "-C", str(odir), "-j4"])
+    if Path("/root/reference/src/comp").is_dir():
+        _run(["make", "-C", str(odir), "ref"])
     return odir / "lib" / "libcomp_oracle.so"
 
 
-def build_all(force: bool = False) -> None:
+def build_all(force: bool = False, asan: bool = False) -> None:
+    """`force` recompiles the product libraries, the C++ drop-in caller and the
+    oracle whatever their timestamps (what __graft_entry__.build() does, so a
+    driver-side build never reuses shipped binaries); the research tools are
+    rebuilt only when stale.  `asan`: also the host-ASan builds (kept out of
+    the GPU push, built on the box by tools/gpu_run.sh asan)."""
     build_mi_reduce(force)
     build_shim(force)
-    build_sweep(force)
-    build_policy_sweep(force)
-    build_fan_sweep(force)
-    build_latency(force)
     build_dropin_caller(force)
-    build_asan(force)
     build_oracle(force)
+    build_sweep()
+    build_policy_sweep()
+    build_fan_sweep()
+    build_latency()
+    if asan:
+        build_asan(force)
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if "--asan" in sys.argv:
+        build_mi_reduce()
+        build_shim()
+        build_asan("--force" in sys.argv)
+    else:
+        build_all(force="--force" in sys.argv)

@@ -422,6 +422,37 @@ ccl::status ccl_comp_reduce(ccl_sched* /*sched*/, const void* in_buf, size_t in_
     return comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
 }
 
+// The reference's keep-precision algorithm as written (comp.cpp:214-234):
+// acc = fp32(inout); for every input i >= 1: tmp = fp32(in_i), then
+// ccl_comp_reduce_regular(tmp -> acc) on float32 (a user callback for custom);
+// finally inout = bf16(acc) with the impl's rounding and truncated count%16
+// tail.  Used where the fused kernel does not apply: a custom reduction, or
+// more inputs than one fused pass takes (MI_MAX_INPUTS).  `tmp` / `acc` are
+// the caller's fp32 scratch of in_count floats (host or device), as in the
+// reference's signature; host scratch is allocated when they are absent.
+static void keep_precision_chain(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
+                                 void* inout_buf, size_t* out_count, size_t es, ccl::reduction reduction,
+                                 ccl::reduction_fn reduction_fn, const ccl::fn_context* context, float* tmp,
+                                 float* acc) {
+    std::vector<float> htmp, hacc;
+    if (!tmp) {
+        htmp.resize(in_count);
+        tmp = htmp.data();
+    }
+    if (!acc) {
+        hacc.resize(in_count);
+        acc = hacc.data();
+    }
+    const ccl_datatype f32(ccl::datatype::float32, sizeof(float));
+    ccl_convert_bf16_to_fp32_arrays(inout_buf, acc, in_count);
+    for (size_t i = 1; i < offsets.size(); i++) {
+        ccl_convert_bf16_to_fp32_arrays(const_cast<char*>(static_cast<const char*>(in_buf)) + es * offsets[i], tmp,
+                                        in_count);
+        comp_reduce_regular(tmp, in_count, acc, out_count, f32, reduction, reduction_fn, context);
+    }
+    ccl_convert_fp32_to_bf16_arrays(acc, inout_buf, in_count);
+}
+
 // ccl_comp_batch_reduce's body, with the issue of each fused fold (`issue(ins,
 // k, out, count, dtype, op, flags)`) left to the caller: synchronous
 // (mi_reduce_multi_sync) or asynchronous (mi_reduce_start, one request per
@@ -431,18 +462,22 @@ template <typename Issue>
 static void batch_reduce_body(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
                               void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
                               ccl::reduction reduction, ccl::reduction_fn reduction_fn,
-                              const ccl::fn_context* context, int bf16_keep_precision_mode, Issue&& issue) {
-    // The fp32 scratch `tmp`/`acc` of the reference (comp.cpp:210-234) is not
-    // needed: the kernel keeps the fp32 accumulator in registers.
+                              const ccl::fn_context* context, int bf16_keep_precision_mode, float* tmp,
+                              float* acc, Issue&& issue) {
+    // Up to MI_MAX_INPUTS inputs the fp32 scratch `tmp`/`acc` of the
+    // reference (comp.cpp:210-234) is not needed: the kernel keeps the fp32
+    // accumulator in registers and rounds once.
     const size_t es = dtype.size();
     if (bf16_keep_precision_mode) {
         // keep-precision: buffers read as bf16 whatever dtype says; inputs
         // strided by dtype.size() (comp.cpp:214-234)
-        if (reduction == ccl::reduction::custom)
-            MI_CCL_THROW("custom reduction is not supported in bf16 keep-precision mode");
         const size_t k = std::max<size_t>(offsets.size(), 1);
-        if (k > MI_MAX_INPUTS) MI_CCL_THROW("keep-precision fan-in supports at most 16 inputs");
         if (in_count == 0) return;
+        if (reduction == ccl::reduction::custom || k > MI_MAX_INPUTS) {
+            keep_precision_chain(in_buf, offsets, in_count, inout_buf, out_count, es, reduction, reduction_fn,
+                                 context, tmp, acc);
+            return;
+        }
         std::vector<const void*> ins(k);
         ins[0] = inout_buf;
         for (size_t i = 1; i < k; i++) ins[i] = static_cast<const char*>(in_buf) + es * offsets[i];
@@ -480,11 +515,11 @@ static void batch_reduce_body(const void* in_buf, const std::vector<size_t>& off
 ccl::status ccl_comp_batch_reduce(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
                                   void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
                                   ccl::reduction reduction, ccl::reduction_fn reduction_fn,
-                                  const ccl::fn_context* context, int bf16_keep_precision_mode, float* /*tmp*/,
-                                  float* /*acc*/) {
+                                  const ccl::fn_context* context, int bf16_keep_precision_mode, float* tmp,
+                                  float* acc) {
     TraceRange range("comp_batch_reduce");
     batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
-                      bf16_keep_precision_mode,
+                      bf16_keep_precision_mode, tmp, acc,
                       [](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
                           check(fold_sync(ins, k, out, n, dt, op, f), "mi_reduce_multi_sync");
                       });
@@ -544,8 +579,10 @@ ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<si
             }
         }
     } drop{q.get()};
+    // (a keep-precision chain — custom op, > MI_MAX_INPUTS inputs — completes
+    // inside this call, as a custom reduction does in ccl_comp_reduce_start)
     batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
-                      bf16_keep_precision_mode,
+                      bf16_keep_precision_mode, nullptr, nullptr,
                       [&](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
                           mi_request_t r = nullptr;
                           check(mi_reduce_start(ins, k, out, n, dt, op, f, mi_comp_device(), &r), "mi_reduce_start");
@@ -623,6 +660,17 @@ int mi_ccl_comp_batch_reduce(const void* in_buf, const size_t* offsets, size_t n
         std::vector<size_t> offs(offsets, offsets + n_offsets);
         return (int)ccl_comp_batch_reduce(in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
                                           static_cast<ccl::reduction>(op), nullptr, nullptr,
+                                          bf16_keep_precision_mode, nullptr, nullptr);
+    });
+}
+
+int mi_ccl_comp_batch_reduce_custom(const void* in_buf, const size_t* offsets, size_t n_offsets, size_t in_count,
+                                    void* inout_buf, size_t* out_count, int dtype, int bf16_keep_precision_mode,
+                                    mi_ccl_reduction_fn fn) {
+    MI_SHIM_GUARD({
+        std::vector<size_t> offs(offsets, offsets + n_offsets);
+        return (int)ccl_comp_batch_reduce(in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
+                                          ccl::reduction::custom, reinterpret_cast<ccl::reduction_fn>(fn), nullptr,
                                           bf16_keep_precision_mode, nullptr, nullptr);
     });
 }

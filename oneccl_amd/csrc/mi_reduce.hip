@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <sched.h>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -411,6 +412,15 @@ int check_batch_disjoint(const mi_reduce_desc_t* d, int n, size_t es) {
         uintptr_t lo, hi;
         int owner;
     };
+    // A range end lo + count * es must not wrap: a corrupt count would
+    // otherwise pass the overlap test below with an end below its start.
+    for (int i = 0; i < n; i++) {
+        if (!d[i].count) continue;
+        const uintptr_t lim = UINTPTR_MAX / es;
+        const uintptr_t lo_in = reinterpret_cast<uintptr_t>(d[i].in), lo_io = reinterpret_cast<uintptr_t>(d[i].inout);
+        if (d[i].count > lim || d[i].count * es > UINTPTR_MAX - lo_in || d[i].count * es > UINTPTR_MAX - lo_io)
+            return fail(MI_E_INVALID, "batch descriptor count overflows the address space");
+    }
     std::vector<Rng> outs;
     outs.reserve(n);
     for (int i = 0; i < n; i++)
@@ -611,17 +621,24 @@ thread_local ThreadCtx t_ctx;
 int get_ctx(int device, DevCtx** out) {
     if (device < 0) MI_HIP(hipGetDevice(&device));
     if ((size_t)device >= t_ctx.devs.size()) t_ctx.devs.resize(device + 1, nullptr);
-    DevCtx*& d = t_ctx.devs[device];
-    if (!d) {
+    if (!t_ctx.devs[device]) {
+        // Built in full before it is published: a failure leaves no
+        // half-made context (a null stream would be the legacy default
+        // stream) cached for the thread, and the caller's device is restored
+        // on every path.
         int prev = 0;
         MI_HIP(hipGetDevice(&prev));
+        struct Restore {
+            int dev;
+            ~Restore() { (void)hipSetDevice(dev); }
+        } restore{prev};
         MI_HIP(hipSetDevice(device));
-        d = new DevCtx();
+        std::unique_ptr<DevCtx> d(new DevCtx());
         d->device = device;
         for (int s = 0; s < 2; s++) MI_HIP(hipStreamCreateWithFlags(&d->stream[s], hipStreamNonBlocking));
-        MI_HIP(hipSetDevice(prev));
+        t_ctx.devs[device] = d.release();
     }
-    *out = d;
+    *out = t_ctx.devs[device];
     return 0;
 }
 
@@ -862,6 +879,11 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
 // pipeline (drain thread included), with its own streams and staging buffers
 // that persist across requests.
 struct AsyncJob {
+    // Work the calling thread had already issued on its own streams when the
+    // job was submitted: the worker waits for it first, so a staged request
+    // never overtakes an earlier direct one (e.g. a device-only reduce that
+    // writes an operand this job reads).
+    std::vector<hipEvent_t> prior;
     const void* inputs[MI_MAX_INPUTS];
     int k = 0;
     void* out = nullptr;
@@ -880,6 +902,9 @@ struct AsyncJob {
         cv.wait(lk, [&] { return done; });
         return rc;
     }
+    ~AsyncJob() {
+        for (hipEvent_t e : prior) (void)hipEventDestroy(e);  // a job that never ran
+    }
 };
 
 struct StageWorker {
@@ -887,15 +912,35 @@ struct StageWorker {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::shared_ptr<AsyncJob>> q;
+    size_t inflight = 0;  // submitted and not yet finished (guarded by mu)
     bool stop = false;
 
     void submit(const std::shared_ptr<AsyncJob>& j) {
         {
             std::lock_guard<std::mutex> lk(mu);
             q.push_back(j);
+            inflight++;
         }
-        if (!th.joinable()) th = std::thread([this] { loop(); });
+        if (!th.joinable()) {
+            try {
+                th = std::thread([this] { loop(); });
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu);
+                q.pop_back();
+                inflight--;
+                throw;
+            }
+        }
         cv.notify_all();
+    }
+    bool busy() {
+        std::lock_guard<std::mutex> lk(mu);
+        return inflight != 0;
+    }
+    // Wait until every submitted job has finished (their results are final).
+    void wait_idle() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return inflight == 0; });
     }
     void loop() {
         for (;;) {
@@ -907,12 +952,24 @@ struct StageWorker {
                 j = q.front();
                 q.pop_front();
             }
-            const int rc = reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags, j->device);
-            std::lock_guard<std::mutex> lk(j->mu);
-            j->rc = rc;
-            if (rc) j->err = g_last_error;  // the worker's thread-local message
-            j->done = true;
-            j->cv.notify_all();
+            int rc = 0;
+            for (hipEvent_t e : j->prior) {
+                const hipError_t he = hipEventSynchronize(e);
+                if (he != hipSuccess && !rc) rc = hip_fail(he, "waiting for earlier work of the submitting thread");
+                (void)hipEventDestroy(e);
+            }
+            j->prior.clear();
+            if (!rc) rc = reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags, j->device);
+            {
+                std::lock_guard<std::mutex> lk(j->mu);
+                j->rc = rc;
+                if (rc) j->err = g_last_error;  // the worker's thread-local message
+                j->done = true;
+                j->cv.notify_all();
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            inflight--;
+            cv.notify_all();
         }
     }
     // Thread exit: finish every submitted job (they write the callers'
@@ -928,6 +985,38 @@ struct StageWorker {
     }
 };
 thread_local StageWorker t_stage;
+
+// Events behind the work the calling thread has queued on its own streams
+// (every device it used); streams that are already idle need none.
+std::vector<hipEvent_t> record_prior() {
+    std::vector<hipEvent_t> evs;
+    int prev = -1;
+    for (DevCtx* d : t_ctx.devs) {
+        if (!d) continue;
+        for (int s = 0; s < 2; s++) {
+            if (!d->stream[s]) continue;
+            const hipError_t q = hipStreamQuery(d->stream[s]);
+            if (q == hipSuccess) continue;
+            (void)hipGetLastError();
+            if (prev < 0 && hipGetDevice(&prev) != hipSuccess) prev = -1;
+            hipEvent_t e = nullptr;
+            if (hipSetDevice(d->device) != hipSuccess ||
+                hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                for (hipEvent_t x : evs) (void)hipEventDestroy(x);
+                if (prev >= 0) (void)hipSetDevice(prev);
+                throw std::runtime_error("cannot create an ordering event");
+            }
+            if (hipEventRecord(e, d->stream[s]) != hipSuccess) {
+                (void)hipEventDestroy(e);
+                (void)hipStreamSynchronize(d->stream[s]);  // order by waiting instead
+                continue;
+            }
+            evs.push_back(e);
+        }
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return evs;
+}
 
 // Does a fold over these operands need host staging (pageable operands, or
 // pinned ones under MI_HOST_STAGED)?
@@ -1041,6 +1130,7 @@ int mi_reduce_batch(const mi_reduce_desc_t* descs, int n, int dtype, int op, uns
 int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,
                    int device) {
     return guarded([&]() -> int {
+        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         const void* ins[2] = {inout, in};
         return reduce_sync(ins, 2, inout, count, dtype, op, flags, device);
     });
@@ -1049,6 +1139,7 @@ int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op,
 int mi_reduce_multi_sync(const void* const* inputs, int k, void* out, size_t count, int dtype,
                          int op, unsigned flags, int device) {
     return guarded([&]() -> int {
+        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         if (!inputs) return fail(MI_E_INVALID, "null input list");
         return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
     });
@@ -1062,6 +1153,7 @@ int mi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t 
 int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags,
                     int device) {
     return guarded([&]() -> int {
+        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         if (!pick_conv(src_dtype, dst_dtype, flags))
             return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
         if (count == 0) return 0;
@@ -1140,8 +1232,13 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
                 if (!inputs[i]) return fail(MI_E_INVALID, "null input");
             if (op < MI_OP_SUM || op > MI_OP_MAX)
                 return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
-            if (needs_staging(inputs, k, out)) {
+            // Staged work runs on the calling thread's worker.  While that
+            // worker still has requests of this thread, later requests go
+            // there too, so a thread's requests run in submission order
+            // whatever their pointer kinds.
+            if (needs_staging(inputs, k, out) || t_stage.busy()) {
                 auto j = std::make_shared<AsyncJob>();
+                j->prior = record_prior();
                 for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
                 j->k = k;
                 j->out = out;
@@ -1229,6 +1326,7 @@ int mi_request_free(mi_request_t req) {
 int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
                                  unsigned flags, int nshards, const int* devices) {
     return guarded([&]() -> int {
+        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         if (!inputs || !devices || nshards < 1) return fail(MI_E_INVALID, "bad shard arguments");
         if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
         const size_t es = dtype_size(dtype);
@@ -1242,6 +1340,14 @@ int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, si
         while ((int)t_shard_workers.size() < nshards - 1) t_shard_workers.emplace_back(new StageWorker());
         const size_t per = ((count + (size_t)nshards - 1) / (size_t)nshards + 255) / 256 * 256;
         std::vector<std::shared_ptr<AsyncJob>> jobs;
+        // Every shard already submitted finishes before this call returns on
+        // any path, a throw included: they write the caller's `out`.
+        struct WaitAll {
+            std::vector<std::shared_ptr<AsyncJob>>& jobs;
+            ~WaitAll() {
+                for (auto& j : jobs) (void)j->wait();
+            }
+        } wait_all{jobs};
         for (int sh = 1; sh < nshards; sh++) {
             const size_t b = std::min(count, per * (size_t)sh), e = std::min(count, b + per);
             if (b >= e) break;
@@ -1254,8 +1360,13 @@ int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, si
             j->op = op;
             j->flags = flags;
             j->device = devices[sh];
-            t_shard_workers[sh - 1]->submit(j);
             jobs.push_back(j);
+            try {
+                t_shard_workers[sh - 1]->submit(j);
+            } catch (...) {
+                jobs.pop_back();  // never queued: nothing to wait for
+                throw;
+            }
         }
         const int rc0 = reduce_sync(inputs, k, out, std::min(count, per), dtype, op, flags, devices[0]);
         std::string err0 = rc0 ? g_last_error : std::string();
@@ -1330,6 +1441,7 @@ int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* str
 
 int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int device) {
     return guarded([&]() -> int {
+        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         if (bytes == 0) return 0;
         if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
         int pdev = -1;

@@ -165,10 +165,25 @@ uint16_t orc_fp32_to_fp16_rne(float f) {
  * (so `inout` on NaN and on +0/-0 ties); MAXPS likewise with >.
  * bf16_intrisics.cpp:28-34, fp16_intrisics.hpp:72-77.  Non-simd = std::
  * forms of bf16.cpp:42-48. */
+/* x86 NaN propagation of ADDPS/MULPS (Intel SDM vol. 1 §4.8.3.5, table
+ * 4-7): a NaN operand is returned quieted, the FIRST source's when both are
+ * NaN; an invalid operation on non-NaN operands (inf - inf, 0 * inf) gives the
+ * default NaN, which the C operation below already produces on x86.  The
+ * reference computes _mm512_add_ps(in, inout) (bf16_intrisics.cpp:20-26,
+ * fp16_intrisics.hpp:58-63), so `in` is the first source.  Pinned bit for bit,
+ * payloads included, by tests/golden/ref_vectors.npz (the reference's own
+ * code, oracle/ref_harness.cpp).  C's `in + io` alone leaves the both-NaN
+ * choice to the compiler's operand order. */
+static inline float x86_nan_first(float r, float first, float second) {
+    if (first != first) return u2f(f2u(first) | 0x400000u);
+    if (second != second) return u2f(f2u(second) | 0x400000u);
+    return r;
+}
+
 static inline float lp_apply(int op, int simd, float in, float io) {
     switch (op) {
-        case OP_SUM: return in + io;
-        case OP_PROD: return in * io;
+        case OP_SUM: return x86_nan_first(in + io, in, io);
+        case OP_PROD: return x86_nan_first(in * io, in, io);
         case OP_MIN: return simd ? ((in < io) ? in : io) : ((io < in) ? io : in);
         default: return simd ? ((in > io) ? in : io) : ((in < io) ? io : in);
     }

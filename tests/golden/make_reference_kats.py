@@ -12,7 +12,7 @@ Sources (reference snapshot 2024-12-20):
   tests/functional/test_impl.hpp:268-320   closed-form expected values (computed in T / float)
   tests/functional/test_impl.hpp:160-204   tolerance g = log2(P)*eps / (1 - log2(P)*eps), max_error = g*expected
   tests/functional/lp.hpp:32-35            eps: 2^-10 fp16 (x2), 2^-23 fp32, 2^-52 fp64, 2^-7 bf16 (x2)
-  tests/functional/conf.cpp:51-53,59       sizes 17 / 32771 / 262144 elements, buffer counts 1 and 4
+  tests/functional/conf.cpp:51-53,59       sizes 17 / 32771 / 262144 (SIZE_SMALL/MEDIUM/LARGE), buffer counts 1 and 4
   examples/cpu/cpu_allreduce_bf16_test.cpp:29-50,80-97   bf16 allreduce of rank+idx, eps 2^-7 (x1)
   examples/benchmark/src/allreduce/cpu_allreduce_coll.hpp:29-57 + include/coll.hpp:152-170  fill = rank,
                                            expected (P-1)*P/2
@@ -98,7 +98,7 @@ def main():
                         fill = f"{c1}*r + {c2}*b + (op == prod)"
                         tol = abs(max_error(dt, P, exp))
                     cases.append({"suite": "tests/functional", "dtype": dt, "op": op, "P": P, "buf_idx": b,
-                                  "counts": [17, 32771], "fill": fill, "coeff": list(COEFF.get(dt, (1.0, 1.0))),
+                                  "counts": [17, 32771, 262144], "fill": fill, "coeff": list(COEFF.get(dt, (1.0, 1.0))),
                                   "expected": exp, "max_error": tol})
     # examples/cpu/cpu_allreduce_bf16_test.cpp: value rank+idx, bf16 sum, eps 2^-7
     for P in (2, 4, 8):

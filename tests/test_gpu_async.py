@@ -228,3 +228,53 @@ def test_multi_sync_sharded_same_bits(where, nshards):
     else:
         got = out
     assert_same(got, ref_out, BF16, f"{where} x{nshards}")
+
+
+@pytest.mark.parametrize("first", ["staged", "direct"])
+def test_staged_and_direct_requests_keep_submission_order(first):
+    """Requests of one thread run in submission order whatever their pointer
+    kinds: a staged request (pageable operands, run by the thread's worker)
+    and a device-only request (launched on the thread's stream) that reads
+    the other's output, in both orders; then a synchronous call that reads
+    the last output."""
+    import torch
+    m = _lib.mi()
+    n = (64 << 20) // 4
+    a = rand_array(FP32, n, seed=21, specials=False)
+    h = rand_array(FP32, n, seed=22, specials=False)  # pageable
+    d0 = rand_array(FP32, n, seed=23, specials=False)
+    td, pd = to_dev(d0)
+    torch.cuda.synchronize()
+    reqs = []
+
+    def start(ins, out):
+        r = ctypes.c_void_p()
+        _lib.check(m.mi_reduce_start(_lib.void_ptr_array(ins), 2, out, n, FP32, 0, 0, -1, ctypes.byref(r)))
+        reqs.append(r)
+
+    ta, pa = to_dev(a)
+    torch.cuda.synchronize()
+    exp_h, exp_d = h.copy(), d0.copy()
+    if first == "staged":
+        # h += a (staged: pageable h), then d += h (device d reads pageable h: staged)... then d += a on device
+        start([h.ctypes.data, pa], h.ctypes.data)
+        oracle.comp_reduce(a, exp_h, FP32, 0)
+        start([pd, pa], pd)  # device-only: must wait for nothing but keeps order
+        oracle.comp_reduce(a, exp_d, FP32, 0)
+        start([pd, h.ctypes.data], pd)  # reads the staged request's output
+        oracle.comp_reduce(exp_h, exp_d, FP32, 0)
+    else:
+        start([pd, pa], pd)  # device-only, queued on the thread's stream
+        oracle.comp_reduce(a, exp_d, FP32, 0)
+        start([h.ctypes.data, pd], h.ctypes.data)  # staged: reads the device request's output
+        oracle.comp_reduce(exp_d, exp_h, FP32, 0)
+        start([pd, pa], pd)  # device-only again, after a staged one
+        oracle.comp_reduce(a, exp_d, FP32, 0)
+    # synchronous call on the same thread: runs after every request above
+    _lib.check(m.mi_reduce_sync(pd, h.ctypes.data, n, FP32, 0, 0, -1))
+    oracle.comp_reduce(exp_d, exp_h, FP32, 0)
+    for r in reqs:
+        _lib.check(m.mi_wait(r))
+        _lib.check(m.mi_request_free(r))
+    assert_same(from_dev(td, d0), exp_d, FP32, "device operand")
+    assert_same(h, exp_h, FP32, "pageable operand")

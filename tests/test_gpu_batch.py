@@ -142,3 +142,18 @@ def test_batch_refuses_overlap():
     # adjacent, touching ranges and a shared input are fine
     assert m.mi_reduce_batch(_lib.desc_array([(p, p + 4096, 100), (p, p + 4096 + 400, 100)]), 2, FP32, 0, 0, s) == 0
     torch.cuda.synchronize()
+
+
+def test_batch_refuses_wrapping_count():
+    """A count whose byte range would wrap past the end of the address space
+    is refused (MI_E_INVALID), not launched."""
+    import torch
+    m = _lib.mi()
+    t = torch.zeros(1 << 12, dtype=torch.float32, device="cuda")
+    p = t.data_ptr()
+    s = torch.cuda.current_stream().cuda_stream
+    huge = (1 << 64) // 4 - 1
+    assert m.mi_reduce_batch(_lib.desc_array([(p, p + 4096, 16), (p + 8192, p + 12288, huge)]), 2, FP32, 0, 0,
+                             s) == -1
+    assert b"overflow" in m.mi_last_error()
+    torch.cuda.synchronize()

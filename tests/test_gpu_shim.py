@@ -198,8 +198,8 @@ def test_bf16_fp16_entry_points():
 @pytest.mark.parametrize("k", [1, 2, 5, 16, 23])
 @pytest.mark.parametrize("dt", [BF16, FP32, FP16])
 def test_comp_batch_reduce(keep, k, dt):
-    if keep and k > 16:
-        pytest.skip("keep-precision fan-in is bounded at 16 inputs")
+    """Storage-precision folds chain groups of 16; keep-precision past 16
+    inputs runs the reference's fp32 scratch chain (comp.cpp:214-234)."""
     if keep and dt != BF16:
         pytest.skip("keep-precision mode reads bf16")
     n = 4099
@@ -367,8 +367,10 @@ def test_cpp_caller_under_host_asan():
     from pathlib import Path
     exe = Path(__file__).resolve().parent / "cpp" / "dropin_caller_asan"
     if not exe.exists():
-        from oneccl_amd import build
-        build.build_asan()
+        # The ASan builds stay out of the GPU push (.gpurunignore); they are
+        # built on the box by `tools/gpu_run.sh asan` (python -m
+        # oneccl_amd.build --asan) before this test runs there.
+        pytest.skip("host-ASan build absent: run `python -m oneccl_amd.build --asan` first")
     # quarantine_size_mb=0: ROCm's ASan runtime tracks pinned host memory
     # (hipHostMalloc) in its device allocator, and a freed pinned chunk still
     # in quarantine when libamdhip64 unloads at exit trips the runtime's own
@@ -560,7 +562,7 @@ def test_roctx_range_around_reduce(tmp_path):
 
 @pytest.mark.parametrize("where", ["device", "pageable"])
 @pytest.mark.parametrize("dt,op,k,keep", [(FP32, 0, 5, 0), (FP32, 3, 23, 0), (BF16, 0, 4, 1), (BF16, 2, 9, 0),
-                                          (4, 1, 17, 0), (FP16, 0, 3, 0)])
+                                          (4, 1, 17, 0), (FP16, 0, 3, 0), (BF16, 3, 19, 1)])
 def test_comp_batch_reduce_start_matches_sync(where, dt, op, k, keep):
     """ccl_comp_batch_reduce_start (one request; chained launches past 16
     inputs) gives the bits and out_count of the synchronous
@@ -698,3 +700,72 @@ def test_shard_devices_env(dt):
         finally:
             os.environ.pop("CCL_COMP_HIP_SHARD_DEVICES", None)
             comp.env_reload()
+
+
+@pytest.mark.parametrize("where", ["device", "pageable"])
+@pytest.mark.parametrize("k,op", [(17, 0), (33, 2), (20, 3)])
+def test_keep_precision_past_16_inputs(where, k, op):
+    """ccl_comp_batch_reduce(bf16_keep_precision_mode=1) with more inputs than
+    one fused pass takes: the fp32 scratch chain of the reference (convert,
+    float32 reduce per input, one final rounding) against the oracle's
+    restatement of comp.cpp:214-234, under the impl in force, with the
+    caller's tmp/acc scratch absent (host scratch is allocated)."""
+    b_impl, _ = impls()
+    n = 4099  # count % 16 == 3: the truncated tail of the final conversion
+    ins = [rand_array(BF16, n, seed=800 + j, op=op) for j in range(k)]
+    packed = np.concatenate(ins)
+    offsets = [j * n for j in range(k)]
+    exp = ins[0].copy()
+    oracle.batch_reduce(packed, offsets, n, exp, BF16, op, 1, b_impl, 0)
+    if where == "device":
+        tp, pp = to_dev(packed)
+        to, po = to_dev(ins[0])
+    else:
+        host = ins[0].copy()
+        pp, po = ptr(packed), ptr(host)
+    oc = comp.comp_batch_reduce(pp, offsets, n, po, comp.datatype.bfloat16, comp.reduction(op), 1)
+    got = from_dev(to, exp) if where == "device" else host
+    assert_same(got, exp, BF16, f"k={k}")
+    assert oc is None  # float32 CCL_REDUCE steps never write out_count
+
+
+def test_keep_precision_custom_reduction():
+    """keep-precision with reduction::custom: the user's callback runs on the
+    fp32 scratch once per input, with datatype float32, and the result is
+    rounded to bf16 once at the end (comp.cpp:214-234)."""
+    calls = []
+
+    def fn(in_p, count, inout_p, out_count_p, dtype, ctx):
+        calls.append(dtype)
+        src = np.ctypeslib.as_array(ctypes.cast(in_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst = np.ctypeslib.as_array(ctypes.cast(inout_p, ctypes.POINTER(ctypes.c_float)), (count,))
+        dst[:] = np.maximum(dst, src) + np.float32(0.001)
+
+    cb = _lib.MI_CCL_REDUCTION_FN(fn)
+    n, k = 67, 3
+    ins = [oracle.f32_to_bf16(np.linspace(j, j + 1, n, dtype=np.float32), True) for j in range(k)]
+    packed = np.concatenate(ins)
+    offs = (ctypes.c_size_t * k)(*[j * n for j in range(k)])
+    b_impl, _ = impls()
+    acc = oracle.bf16_to_f32(ins[0]).copy()
+    for j in range(1, k):
+        acc = np.maximum(acc, oracle.bf16_to_f32(ins[j])) + np.float32(0.001)
+    exp = np.empty(n, np.uint16)
+    oracle.lib().orc_convert_fp32_to_bf16_arrays(acc.ctypes.data, exp.ctypes.data, n, b_impl)
+    for where in ("host", "device"):
+        calls.clear()
+        if where == "host":
+            got = ins[0].copy()
+            pp, po = ptr(packed), ptr(got)
+        else:
+            tp, pp = to_dev(packed)
+            to, po = to_dev(ins[0])
+        _lib.check_shim(_lib.shim().mi_ccl_comp_batch_reduce_custom(pp, offs, k, n, po, None, BF16, 1, cb))
+        if where == "device":
+            got = from_dev(to, exp)
+        assert calls == [FP32] * (k - 1)
+        assert_same(got, exp, BF16, where)
+    null_fn = ctypes.cast(None, _lib.MI_CCL_REDUCTION_FN)
+    assert _lib.shim().mi_ccl_comp_batch_reduce_custom(ptr(packed), offs, k, n, ptr(ins[0].copy()), None, BF16, 1,
+                                                       null_fn) == -1
+    assert b"callback" in _lib.shim().mi_ccl_last_error()

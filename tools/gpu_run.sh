@@ -26,11 +26,13 @@ for step in "$@"; do
         host)
             { nproc; lscpu; rocm-smi --showproductname --showmeminfo vram 2>&1 | head -40; } > "$OUT/host.txt" 2>&1 ;;
         tests)
-            run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider ;;
+            run pytest_gpu 1000 python -u -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         tests_fast)
             run pytest_gpu 600 python -m pytest tests -m gpu -q --maxfail=50 -p no:cacheprovider -k "not full" ;;
         asan)
-            ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0 run asan 300 ./tests/cpp/dropin_caller_asan ;;
+            run asan_build 600 python -m oneccl_amd.build --asan &&
+            ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:quarantine_size_mb=0 run asan 300 ./tests/cpp/dropin_caller_asan &&
+            run pytest_asan 300 python -m pytest tests/test_gpu_shim.py -m gpu -q -k asan -p no:cacheprovider ;;
         latency)
             run latency 300 ./tools/latency 2000 ;;
         smoke)
