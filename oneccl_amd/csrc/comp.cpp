@@ -22,8 +22,10 @@
 //                      bench (ccl_mirror.hpp; same mangled symbols).
 #include <dlfcn.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -38,14 +40,33 @@
 #include "comp/comp.hpp"
 #include "comp/fp16/fp16.hpp"
 #define MI_CCL_THROW(msg) CCL_THROW(msg)
+#define MI_CCL_FATAL(msg) CCL_FATAL(msg)
 #include "mi_ccl_comp_async.hpp"  // include/ (on the include path)
 static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
 static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
-static int mi_comp_device() { return -1; }
+// CCL_COMP_HIP_DEVICE: the GPU for operands that name none (host buffers);
+// read once, like the rest of oneCCL's environment (env.cpp reads it at init).
+static int mi_comp_device() {
+    static const int dev = [] {
+        const char* v = getenv("CCL_COMP_HIP_DEVICE");
+        return v ? atoi(v) : -1;
+    }();
+    return dev;
+}
 #else
 #include "../../include/mi_ccl_comp.h"
 #include "ccl_mirror.hpp"
 #define MI_CCL_THROW(msg) throw ccl::exception(msg)
+// CCL_FATAL (src/common/log/log.hpp:333-337): log the error, std::terminate().
+// The reference uses it for an unknown dtype or reduction (comp.cpp:56,113,
+// bf16.cpp:73, bf16_intrisics.hpp:131, fp16_intrisics.hpp:222-243); the
+// standalone build does the same, so a caller sees the reference's behaviour.
+[[noreturn]] static void mi_ccl_fatal(const std::string& msg) {
+    fprintf(stderr, "oneccl_amd: FATAL: %s\n", msg.c_str());
+    fflush(stderr);
+    std::terminate();
+}
+#define MI_CCL_FATAL(msg) mi_ccl_fatal(msg)
 #include "../../include/mi_ccl_comp_async.hpp"
 #endif
 
@@ -195,6 +216,15 @@ bool reduce_semantics(int dt, unsigned* f) {
     return true;
 }
 
+// sum / prod / min / max: the cases of the reference's op switches; any
+// other value (custom included, where it reaches them) is CCL_FATAL there.
+bool builtin_op(ccl::reduction op) {
+    const int v = static_cast<int>(op);
+    return v >= 0 && v <= 3;
+}
+
+std::string unexpected(int v) { return "unexpected value " + std::to_string(v); }
+
 void check(int rc, const char* where) {
     if (rc != 0) MI_CCL_THROW(std::string(where) + " failed: " + mi_last_error());
 }
@@ -294,10 +324,12 @@ std::vector<int> shard_devices() {
     return g_shard_devs;
 }
 
-void shard_env_reload() {
+#ifndef MI_ONECCL_TREE
+void shard_env_reload() {  // standalone only: oneCCL's env is read once, at init
     std::lock_guard<std::mutex> g(g_shard_mu);
     g_shard_ready = false;
 }
+#endif
 
 // The synchronous fold every entry point ends in: one GPU, or, for host
 // operands under CCL_COMP_HIP_SHARD_DEVICES, several.
@@ -343,16 +375,24 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
 
 void ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
     if (out_cnt != nullptr) *out_cnt = in_cnt;
-    if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
+    if (!builtin_op(op)) MI_CCL_FATAL(unexpected(static_cast<int>(op)));  // bf16.cpp:73, bf16_intrisics.hpp:131
     check(reduce2_sync(in_buf, inout_buf, in_cnt, MI_BFLOAT16, static_cast<int>(op), bf16_flags(mi_bf16_impl())),
           "mi_reduce_sync(bf16)");
 }
 
+// bf16.cpp:63-85: the scalar impl's semantics (std::min/max operand order,
+// truncation) whatever impl type is in force; a global symbol of bf16.o.
+void ccl_bf16_reduce_scalar_impl(const void* in_buf, void* inout_buf, size_t in_count, ccl::reduction op) {
+    if (!builtin_op(op)) MI_CCL_FATAL(unexpected(static_cast<int>(op)));  // bf16.cpp:73
+    check(reduce2_sync(in_buf, inout_buf, in_count, MI_BFLOAT16, static_cast<int>(op), bf16_flags(ccl_bf16_scalar)),
+          "mi_reduce_sync(bf16 scalar)");
+}
+
 void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
     if (out_cnt != nullptr) *out_cnt = in_cnt;
-    if (op == ccl::reduction::custom) MI_CCL_THROW("unexpected value 4");
     unsigned f = 0;
-    if (!fp16_flags(mi_fp16_impl(), &f)) return;
+    if (!fp16_flags(mi_fp16_impl(), &f)) return;  // no impl branch taken: nothing computed, no check
+    if (!builtin_op(op)) MI_CCL_FATAL(unexpected(static_cast<int>(op)));  // fp16_intrisics.hpp:222-243
     check(reduce2_sync(in_buf, inout_buf, in_cnt, MI_FLOAT16, static_cast<int>(op), f), "mi_reduce_sync(fp16)");
 }
 
@@ -393,8 +433,9 @@ void ccl_convert_fp16_to_fp32(const void* src, void* dst) {
     check(mi_convert_sync(src, MI_FLOAT16, dst, MI_FLOAT32, 8, 0u, mi_comp_device()), "mi_convert_sync");
 }
 
-// ccl_comp_reduce_regular, comp.cpp:76-121
-static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
+// ccl_comp_reduce_regular, comp.cpp:76-121: a global symbol in the reference too
+// (not declared in comp.hpp), kept with its mangled name for the link closure
+ccl::status ccl_comp_reduce_regular(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
                                        const ccl_datatype& dtype, ccl::reduction reduction,
                                        ccl::reduction_fn reduction_fn, const ccl::fn_context* context) {
     if (reduction == ccl::reduction::custom) {
@@ -402,7 +443,9 @@ static ccl::status comp_reduce_regular(const void* in_buf, size_t in_count, void
         return ccl::status::success;
     }
     const int dt = dtype_id(dtype);
-    if (mi_dtype_size(dt) == 0) MI_CCL_THROW("unexpected value " + std::to_string(dt));
+    if (mi_dtype_size(dt) == 0) MI_CCL_FATAL(unexpected(dt));  // comp.cpp:113
+    if (!builtin_op(reduction) && dt != MI_BFLOAT16 && dt != MI_FLOAT16)
+        MI_CCL_FATAL(unexpected(static_cast<int>(reduction)));  // CCL_REDUCE, comp.cpp:56
     TraceRange range("comp_reduce_regular");
     if (dt == MI_BFLOAT16) {
         ccl_bf16_reduce(in_buf, in_count, inout_buf, out_count, reduction);
@@ -419,7 +462,7 @@ ccl::status ccl_comp_reduce(ccl_sched* /*sched*/, const void* in_buf, size_t in_
                             size_t* out_count, const ccl_datatype& dtype, ccl::reduction reduction,
                             ccl::reduction_fn reduction_fn, const ccl::fn_context* context) {
     if (!in_count) return ccl::status::success;
-    return comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
+    return ccl_comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
 }
 
 // The reference's keep-precision algorithm as written (comp.cpp:214-234):
@@ -448,7 +491,7 @@ static void keep_precision_chain(const void* in_buf, const std::vector<size_t>& 
     for (size_t i = 1; i < offsets.size(); i++) {
         ccl_convert_bf16_to_fp32_arrays(const_cast<char*>(static_cast<const char*>(in_buf)) + es * offsets[i], tmp,
                                         in_count);
-        comp_reduce_regular(tmp, in_count, acc, out_count, f32, reduction, reduction_fn, context);
+        ccl_comp_reduce_regular(tmp, in_count, acc, out_count, f32, reduction, reduction_fn, context);
     }
     ccl_convert_fp32_to_bf16_arrays(acc, inout_buf, in_count);
 }
@@ -473,6 +516,8 @@ static void batch_reduce_body(const void* in_buf, const std::vector<size_t>& off
         // strided by dtype.size() (comp.cpp:214-234)
         const size_t k = std::max<size_t>(offsets.size(), 1);
         if (in_count == 0) return;
+        if (reduction != ccl::reduction::custom && !builtin_op(reduction) && k > 1)
+            MI_CCL_FATAL(unexpected(static_cast<int>(reduction)));  // the float32 CCL_REDUCE step, comp.cpp:56
         if (reduction == ccl::reduction::custom || k > MI_MAX_INPUTS) {
             keep_precision_chain(in_buf, offsets, in_count, inout_buf, out_count, es, reduction, reduction_fn,
                                  context, tmp, acc);
@@ -486,20 +531,24 @@ static void batch_reduce_body(const void* in_buf, const std::vector<size_t>& off
         // avx512f / scalar truncate all (bf16.cpp:130-149)
         unsigned f = MI_F_ACC_FP32;
         if (mi_bf16_impl() == ccl_bf16_avx512bf) f |= MI_F_BF16_RNE | MI_F_BF16_TAIL_TRUNC16;
-        issue(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16, static_cast<int>(reduction), f);
+        // one input: only the conversions run (no reduce step checks the op)
+        issue(ins.data(), (int)k, inout_buf, in_count, MI_BFLOAT16, k == 1 ? MI_OP_SUM : static_cast<int>(reduction), f);
         return;
     }
     if (offsets.size() <= 1 || in_count == 0) return;
     if (reduction == ccl::reduction::custom) {
         for (size_t i = 1; i < offsets.size(); i++)
-            comp_reduce_regular(static_cast<const char*>(in_buf) + es * offsets[i], in_count, inout_buf, out_count,
-                                dtype, reduction, reduction_fn, context);
+            ccl_comp_reduce_regular(static_cast<const char*>(in_buf) + es * offsets[i], in_count, inout_buf,
+                                    out_count, dtype, reduction, reduction_fn, context);
         return;
     }
-    // storage-precision left fold == the reference's chained reduces
+    // storage-precision left fold == the reference's chained reduces, which
+    // check dtype and op on every call (ccl_comp_reduce_regular)
     const int dt = dtype_id(dtype);
+    if (mi_dtype_size(dt) == 0) MI_CCL_FATAL(unexpected(dt));
     unsigned f = 0;
     if (!reduce_semantics(dt, &f)) return;
+    if (!builtin_op(reduction)) MI_CCL_FATAL(unexpected(static_cast<int>(reduction)));
     if ((dt == MI_BFLOAT16 || dt == MI_FLOAT16) && out_count) *out_count = in_count;
     size_t next = 1;
     while (next < offsets.size()) {
@@ -544,7 +593,14 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
             run_custom(in_buf, in_count, inout_buf, out_count, dtype, reduction_fn, context);
         } else {
             const int dt = dtype_id(dtype);
-            if (mi_dtype_size(dt) == 0) MI_CCL_THROW("unexpected value " + std::to_string(dt));
+            if (mi_dtype_size(dt) == 0) MI_CCL_FATAL(unexpected(dt));
+            if (dt == MI_FLOAT16) {
+                unsigned f16 = 0;
+                if (fp16_flags(mi_fp16_impl(), &f16) && !builtin_op(reduction))
+                    MI_CCL_FATAL(unexpected(static_cast<int>(reduction)));
+            } else if (!builtin_op(reduction)) {
+                MI_CCL_FATAL(unexpected(static_cast<int>(reduction)));
+            }
             if ((dt == MI_BFLOAT16 || dt == MI_FLOAT16) && out_count) *out_count = in_count;
             unsigned f = 0;
             if (reduce_semantics(dt, &f)) {

@@ -43,6 +43,20 @@ struct async_reduce_entry {
     }
 };
 
+// MPI user ops (MPI_User_function shape) as src/atl/mpi/atl_mpi_ctx.cpp
+// registers them: bf16_sum_op -> ccl_bf16_reduce(in, *length, inout, nullptr,
+// op) (:87-100, unchanged), and the fp16 op with INTEGRATION.md §2b applied
+// (:58-64, ccl_fp16_reduce instead of the inline CPU body).  MPI calls them
+// from its own progress thread on host buffers.
+typedef void (*mpi_user_fn)(void* in, void* inout, int* length, void* datatype);
+static void bf16_sum_op(void* in, void* inout, int* length, void*) {
+    ccl_bf16_reduce(in, *length, inout, nullptr, ccl::reduction::sum);
+}
+static void fp16_max_op(void* in, void* inout, int* length, void*) {
+    size_t len = *length;
+    ccl_fp16_reduce(in, len, inout, nullptr, ccl::reduction::max);
+}
+
 static int failures = 0;
 #define EXPECT(cond, ...)                         \
     do {                                          \
@@ -253,6 +267,21 @@ int main() {
         EXPECT(z.status == complete, "empty async reduce completes at start");
         for (float* p : dbufs) (void)hipFree(p);
         for (float* p : hbufs) free(p);
+    }
+
+    // MPI user ops, called through function pointers as MPI_Reduce_local /
+    // the MPI progress engine would (host buffers, odd length)
+    {
+        const mpi_user_fn ops[2] = {&bf16_sum_op, &fp16_max_op};
+        int len = 1001;
+        std::vector<uint16_t> in(len, 0x3F80), io(len, 0x4000);  // bf16 1.0 + 2.0
+        ops[0](in.data(), io.data(), &len, nullptr);
+        EXPECT(io[0] == 0x4040 && io[len - 1] == 0x4040, "MPI bf16 sum op %04x", io[0]);
+        std::vector<uint16_t> hin(len, 0x4000), hio(len, 0x3C00);  // fp16 max(2.0, 1.0)
+        hin[7] = 0x7E00;  // NaN in `in`: MAXPS(in, inout) returns inout (fp16_intrisics.hpp:72-77)
+        ops[1](hin.data(), hio.data(), &len, nullptr);
+        EXPECT(hio[0] == 0x4000 && hio[len - 1] == 0x4000 && hio[7] == 0x3C00, "MPI fp16 max op %04x %04x", hio[0],
+               hio[7]);
     }
 
     free(comm_buf);
