@@ -170,6 +170,12 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count,
                     int dtype, int op, unsigned flags, int device,
                     mi_request_t* req);
 int mi_test(mi_request_t req, int* done);
+/* Wait until every request this thread has started with mi_reduce_start has
+ * finished.  The synchronous entry points do this themselves; a caller about
+ * to touch an earlier request's operands on the CPU (the drop-in's host
+ * reduce, include/mi_host_reduce.h) calls it first.  Returns at once for a
+ * thread that never started a request.                                     */
+int mi_thread_sync(void);
 int mi_wait(mi_request_t req);
 int mi_request_free(mi_request_t req);
 

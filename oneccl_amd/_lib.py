@@ -48,6 +48,7 @@ MI_API = [
     ("mi_reduce_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
                                 POINTER(c_void_p)]),
     ("mi_test", c_int, [c_void_p, POINTER(c_int)]),
+    ("mi_thread_sync", c_int, []),
     ("mi_wait", c_int, [c_void_p]),
     ("mi_request_free", c_int, [c_void_p]),
     ("mi_reduce_sharded", c_int, [c_int, POINTER(c_int), POINTER(c_void_p), c_int, POINTER(c_void_p),
@@ -102,6 +103,14 @@ SHIM_API = [
 ]
 
 
+# mirrors include/mi_host_reduce.h (exported by libccl_comp_hip.so)
+HOST_API = [
+    ("mi_host_supported", c_int, []),
+    ("mi_host_reduce", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint]),
+    ("mi_host_convert", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint]),
+]
+
+
 def _bind(lib: ctypes.CDLL, api) -> ctypes.CDLL:
     for name, res, args in api:
         fn = getattr(lib, name)
@@ -123,7 +132,7 @@ def shim() -> ctypes.CDLL:
     global _shim
     if _shim is None:
         mi()
-        _shim = _bind(_load("libccl_comp_hip.so"), SHIM_API)
+        _shim = _bind(_bind(_load("libccl_comp_hip.so"), SHIM_API), HOST_API)
     return _shim
 
 
@@ -157,4 +166,4 @@ def lib_paths() -> list[str]:
 
 
 __all__ = ["mi", "shim", "check", "check_shim", "void_ptr_array", "MiReduceError", "MI_CCL_REDUCTION_FN",
-           "MI_API", "SHIM_API", "lib_paths"]
+           "MI_API", "SHIM_API", "HOST_API", "lib_paths"]

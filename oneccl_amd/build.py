@@ -53,15 +53,32 @@ def build_mi_reduce(force: bool = False) -> Path:
     return out
 
 
+# The host reduce (small host-resident chunks, include/mi_host_reduce.h) is
+# compiled for AVX2 + F16C + FMA; comp.cpp calls it only after
+# mi_host_supported() has checked the CPU.
+HOST_REDUCE_FLAGS = ["-O3", "-mavx2", "-mf16c", "-mfma", "-fPIC", "-Wall", "-Wextra"]
+# its 16-lane bf16/fp16 form, called only on CPUs with AVX-512 (+ AVX512_BF16)
+HOST_REDUCE_AVX512_FLAGS = HOST_REDUCE_FLAGS + ["-mavx512f", "-mavx512bw", "-mavx512vl", "-mavx512bf16"]
+
+
 def build_shim(force: bool = False) -> Path:
     out = LIB / "libccl_comp_hip.so"
-    deps = [CSRC / "comp.cpp", CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_reduce.h",
-            ROOT / "include" / "mi_ccl_comp.h", ROOT / "include" / "mi_ccl_comp_async.hpp", LIB / "libmi_reduce.so"]
+    deps = [CSRC / "comp.cpp", CSRC / "host_reduce.cpp", CSRC / "host_reduce_avx512.cpp", CSRC / "host_lp.hpp",
+            CSRC / "ccl_mirror.hpp", ROOT / "include" / "mi_reduce.h",
+            ROOT / "include" / "mi_ccl_comp.h", ROOT / "include" / "mi_ccl_comp_async.hpp",
+            ROOT / "include" / "mi_host_reduce.h", LIB / "libmi_reduce.so"]
     if force or _stale(out, deps):
         cxx = os.environ.get("CXX", "g++")
+        obj = LIB / "host_reduce.o"
+        obj512 = LIB / "host_reduce_avx512.o"
+        _run([cxx, *HOST_REDUCE_FLAGS, "-std=c++17", "-c", "-o", str(obj), str(CSRC / "host_reduce.cpp")])
+        _run([cxx, *HOST_REDUCE_AVX512_FLAGS, "-std=c++17", "-c", "-o", str(obj512),
+              str(CSRC / "host_reduce_avx512.cpp")])
         _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
-              "-o", str(out), str(CSRC / "comp.cpp"),
+              "-o", str(out), str(CSRC / "comp.cpp"), str(obj), str(obj512),
               f"-L{LIB}", "-lmi_reduce", "-ldl", "-Wl,-rpath,$ORIGIN"])
+        obj.unlink()
+        obj512.unlink()
     return out
 
 
@@ -130,9 +147,12 @@ def build_asan(force: bool = False) -> Path:
         # the same compiler (and so the same ASan runtime) as the hipcc-built pieces
         clang = next((c for c in ("/opt/rocm/lib/llvm/bin/clang++", "/opt/rocm/llvm/bin/clang++")
                       if Path(c).exists()), "clang++")
-        _run([clang, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-fsanitize=address",
-              "-fno-omit-frame-pointer", "-o", str(shim), str(CSRC / "comp.cpp"), f"-L{adir}", "-lmi_reduce",
-              "-Wl,-rpath,$ORIGIN"])
+        h512 = adir / "host_reduce_avx512.o"
+        _run([clang, "-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=address", "-fno-omit-frame-pointer",
+              *HOST_REDUCE_AVX512_FLAGS[1:], "-c", "-o", str(h512), str(CSRC / "host_reduce_avx512.cpp")])
+        _run([clang, "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-fsanitize=address", "-mavx2", "-mf16c",
+              "-mfma", "-fno-omit-frame-pointer", "-o", str(shim), str(CSRC / "comp.cpp"),
+              str(CSRC / "host_reduce.cpp"), str(h512), f"-L{adir}", "-lmi_reduce", "-Wl,-rpath,$ORIGIN"])
     src = ROOT / "tests" / "cpp" / "dropin_caller.cpp"
     out = ROOT / "tests" / "cpp" / "dropin_caller_asan"
     if force or _stale(out, [src, shim]):

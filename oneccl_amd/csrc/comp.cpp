@@ -31,6 +31,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/mi_host_reduce.h"
 #include "../../include/mi_reduce.h"
 
 #ifdef MI_ONECCL_TREE
@@ -53,6 +54,7 @@ static int mi_comp_device() {
     }();
     return dev;
 }
+static size_t mi_host_max_bytes();
 #else
 #include "../../include/mi_ccl_comp.h"
 #include "ccl_mirror.hpp"
@@ -85,6 +87,26 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
     std::make_pair(ccl_fp16_f16c, "f16c"), std::make_pair(ccl_fp16_avx512f, "avx512f"),
     std::make_pair(ccl_fp16_avx512fp16, "avx512fp16")};
 
+// CCL_COMP_HOST_MAX_BYTES=<n>: a reduce whose operands are all host memory
+// (pageable or pinned) and whose bucket is at most n bytes runs on the
+// calling thread's CPU (host_reduce.cpp), as the reference runs every reduce;
+// larger ones and all device operands run on the GPU.  0 = always the GPU.
+// The default is the crossover measured on MI355X.
+static const size_t kHostMaxBytesDefault = 32ull << 20;
+
+static size_t parse_host_max() {
+    if (!mi_host_supported()) return 0;  // no AVX2/F16C: the GPU takes everything
+    const char* v = getenv("CCL_COMP_HOST_MAX_BYTES");
+    return v ? (size_t)strtoull(v, nullptr, 0) : kHostMaxBytesDefault;
+}
+
+#ifdef MI_ONECCL_TREE
+static size_t mi_host_max_bytes() {
+    static const size_t m = parse_host_max();  // read once, like oneCCL's env
+    return m;
+}
+#endif
+
 #ifndef MI_ONECCL_TREE
 // ---------------------------------------------------------------------------
 // standalone environment: the reference's CPUID detection
@@ -97,6 +119,7 @@ struct MiEnv {
     ccl_bf16_impl_type bf16 = ccl_bf16_scalar;
     ccl_fp16_impl_type fp16 = ccl_fp16_no_compiler_support;
     int device = -1;  // CCL_COMP_HIP_DEVICE
+    size_t host_max = 0;  // CCL_COMP_HOST_MAX_BYTES
 };
 
 std::mutex g_env_mu;
@@ -164,6 +187,7 @@ void parse_env_locked() {
     if (fp16_types.find(e.fp16) == fp16_types.end())
         MI_CCL_THROW("unsupported FP16 impl type: " + fp16_impl_names[e.fp16]);
     if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) e.device = atoi(v);
+    e.host_max = parse_host_max();
     g_env = e;
     g_env_ready = true;
 }
@@ -179,6 +203,7 @@ const MiEnv& env() {
 static ccl_bf16_impl_type mi_bf16_impl() { return env().bf16; }
 static ccl_fp16_impl_type mi_fp16_impl() { return env().fp16; }
 static int mi_comp_device() { return env().device; }
+static size_t mi_host_max_bytes() { return env().host_max; }
 #endif  // !MI_ONECCL_TREE
 
 // ---------------------------------------------------------------------------
@@ -331,9 +356,34 @@ void shard_env_reload() {  // standalone only: oneCCL's env is read once, at ini
 }
 #endif
 
-// The synchronous fold every entry point ends in: one GPU, or, for host
-// operands under CCL_COMP_HIP_SHARD_DEVICES, several.
+// Are all these operands host memory (pageable or pinned)?
+bool all_host(const void* const* ptrs, int n, const void* out) {
+    if (is_device_ptr(out)) return false;
+    for (int i = 0; i < n; i++)
+        if (is_device_ptr(ptrs[i])) return false;
+    return true;
+}
+
+// The dispatcher: host-resident buckets up to CCL_COMP_HOST_MAX_BYTES stay on
+// the calling thread's CPU: below the crossover a GPU
+// round trip costs more than the reduce.
+bool host_path(const void* const* ins, int k, const void* out, size_t bytes) {
+    const size_t m = mi_host_max_bytes();
+    return m > 0 && bytes <= m && all_host(ins, k, out);
+}
+
+// the host path runs after this thread's outstanding asynchronous requests,
+// which may still be writing these operands
+int host_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags) {
+    if (int rc = mi_thread_sync()) return rc;
+    return mi_host_reduce(ins, k, out, count, dt, op, flags);
+}
+
+// The synchronous fold every entry point ends in: the calling thread's CPU
+// for small host-resident buckets, otherwise one GPU, or, for host operands
+// under CCL_COMP_HIP_SHARD_DEVICES, several.
 int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags) {
+    if (host_path(ins, k, out, count * mi_dtype_size(dt))) return host_fold(ins, k, out, count, dt, op, flags);
     const std::vector<int> devs = shard_devices();
     if (devs.size() >= 2) {
         bool host = !is_device_ptr(out);
@@ -342,6 +392,16 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
             return mi_reduce_multi_sync_sharded(ins, k, out, count, dt, op, flags, (int)devs.size(), devs.data());
     }
     return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+}
+
+// conversions take the same route: the CPU for small host arrays
+int convert_sync(const void* src, int sdt, void* dst, int ddt, size_t count, unsigned flags) {
+    const void* ins[1] = {src};
+    if (host_path(ins, 1, dst, count * std::max(mi_dtype_size(sdt), mi_dtype_size(ddt)))) {
+        if (int rc = mi_thread_sync()) return rc;
+        return mi_host_convert(src, sdt, dst, ddt, count, flags);
+    }
+    return mi_convert_sync(src, sdt, dst, ddt, count, flags, mi_comp_device());
 }
 
 int reduce2_sync(const void* in, void* inout, size_t count, int dt, int op, unsigned flags) {
@@ -369,6 +429,12 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
     if (bytes == 0) return ccl::status::success;
     if (!in_buf) MI_CCL_THROW("in_buf is null");
     if (!out_buf) MI_CCL_THROW("out_buf is null");
+    const void* src[1] = {in_buf};
+    if (mi_host_max_bytes() > 0 && all_host(src, 1, out_buf)) {  // host to host: a memcpy, as the reference
+        check(mi_thread_sync(), "mi_thread_sync");
+        memcpy(out_buf, in_buf, bytes);
+        return ccl::status::success;
+    }
     check(mi_copy_sync(in_buf, out_buf, bytes, use_nontemporal ? 1 : 0, mi_comp_device()), "mi_copy_sync");
     return ccl::status::success;
 }
@@ -405,32 +471,31 @@ static unsigned bf16_conv_flags() {
 }
 
 void ccl_convert_fp32_to_bf16_arrays(void* fp32_buf, void* bf16_buf, size_t count) {
-    check(mi_convert_sync(fp32_buf, MI_FLOAT32, bf16_buf, MI_BFLOAT16, count, bf16_conv_flags(), mi_comp_device()),
+    check(convert_sync(fp32_buf, MI_FLOAT32, bf16_buf, MI_BFLOAT16, count, bf16_conv_flags()),
           "mi_convert_sync(fp32->bf16)");
 }
 
 void ccl_convert_bf16_to_fp32_arrays(void* bf16_buf, float* fp32_buf, size_t count) {
-    check(mi_convert_sync(bf16_buf, MI_BFLOAT16, fp32_buf, MI_FLOAT32, count, 0u, mi_comp_device()),
-          "mi_convert_sync(bf16->fp32)");
+    check(convert_sync(bf16_buf, MI_BFLOAT16, fp32_buf, MI_FLOAT32, count, 0u), "mi_convert_sync(bf16->fp32)");
 }
 
 // 16-element forms (bf16.cpp:113-128): avx512bf -> RNE, otherwise truncate
 void ccl_convert_fp32_to_bf16(const void* src, void* dst) {
     const unsigned f = mi_bf16_impl() == ccl_bf16_avx512bf ? MI_F_BF16_RNE : 0u;
-    check(mi_convert_sync(src, MI_FLOAT32, dst, MI_BFLOAT16, 16, f, mi_comp_device()), "mi_convert_sync");
+    check(convert_sync(src, MI_FLOAT32, dst, MI_BFLOAT16, 16, f), "mi_convert_sync");
 }
 
 void ccl_convert_bf16_to_fp32(const void* src, void* dst) {
-    check(mi_convert_sync(src, MI_BFLOAT16, dst, MI_FLOAT32, 16, 0u, mi_comp_device()), "mi_convert_sync");
+    check(convert_sync(src, MI_BFLOAT16, dst, MI_FLOAT32, 16, 0u), "mi_convert_sync");
 }
 
 // 8-element forms (fp16.cpp:55-61): VCVTPS2PH RNE / VCVTPH2PS
 void ccl_convert_fp32_to_fp16(const void* src, void* dst) {
-    check(mi_convert_sync(src, MI_FLOAT32, dst, MI_FLOAT16, 8, 0u, mi_comp_device()), "mi_convert_sync");
+    check(convert_sync(src, MI_FLOAT32, dst, MI_FLOAT16, 8, 0u), "mi_convert_sync");
 }
 
 void ccl_convert_fp16_to_fp32(const void* src, void* dst) {
-    check(mi_convert_sync(src, MI_FLOAT16, dst, MI_FLOAT32, 8, 0u, mi_comp_device()), "mi_convert_sync");
+    check(convert_sync(src, MI_FLOAT16, dst, MI_FLOAT32, 8, 0u), "mi_convert_sync");
 }
 
 // ccl_comp_reduce_regular, comp.cpp:76-121: a global symbol in the reference too
@@ -605,6 +670,11 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
             unsigned f = 0;
             if (reduce_semantics(dt, &f)) {
                 const void* ins[2] = {inout_buf, in_buf};
+                if (host_path(ins, 2, inout_buf, in_count * mi_dtype_size(dt))) {  // completes here
+                    check(host_fold(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f), "host reduce");
+                    *req = q.release();
+                    return ccl::status::success;
+                }
                 mi_request_t r = nullptr;
                 check(mi_reduce_start(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f,
                                       mi_comp_device(), &r),
@@ -640,6 +710,10 @@ ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<si
     batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
                       bf16_keep_precision_mode, nullptr, nullptr,
                       [&](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
+                          if (host_path(ins, k, out, n * mi_dtype_size(dt))) {  // small host bucket: done here
+                              check(host_fold(ins, k, out, n, dt, op, f), "host reduce");
+                              return;
+                          }
                           mi_request_t r = nullptr;
                           check(mi_reduce_start(ins, k, out, n, dt, op, f, mi_comp_device(), &r), "mi_reduce_start");
                           q->r.push_back(r);

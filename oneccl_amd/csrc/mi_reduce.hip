@@ -985,6 +985,9 @@ struct StageWorker {
     }
 };
 thread_local StageWorker t_stage;
+// This thread has started asynchronous requests that mi_thread_sync has not
+// yet waited for.
+thread_local bool t_async_issued = false;
 
 // Events behind the work the calling thread has queued on its own streams
 // (every device it used); streams that are already idle need none.
@@ -1224,6 +1227,7 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
         if (!req) return fail(MI_E_INVALID, "null request pointer");
         *req = nullptr;
         if (!inputs) return fail(MI_E_INVALID, "null input list");
+        t_async_issued = true;
         if (!dtype_size(dtype)) return fail(MI_E_INVALID, "unknown datatype");
         if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
         if (count > 0) {
@@ -1464,6 +1468,20 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
         }
         MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
         MI_HIP(wait_stream(d->stream[0]));
+        return 0;
+    });
+}
+
+int mi_thread_sync(void) {
+    return guarded([&]() -> int {
+        if (!t_async_issued) return 0;
+        t_stage.wait_idle();
+        for (DevCtx* d : t_ctx.devs) {
+            if (!d) continue;
+            for (int s = 0; s < 2; s++)
+                if (d->stream[s]) MI_HIP(hipStreamSynchronize(d->stream[s]));
+        }
+        t_async_issued = false;
         return 0;
     });
 }

@@ -78,7 +78,7 @@ def test_conversion_matches_reference_stores(impl, f, exp):
 @pytest.fixture
 def impl_env():
     """Set CCL_BF16 / CCL_FP16 for the drop-in, restore afterwards."""
-    saved = {k: os.environ.get(k) for k in ("CCL_BF16", "CCL_FP16")}
+    saved = {k: os.environ.get(k) for k in ("CCL_BF16", "CCL_FP16", "CCL_COMP_HOST_MAX_BYTES")}
 
     def set_(name, value):
         os.environ[name] = value
@@ -93,14 +93,16 @@ def impl_env():
     comp.env_reload()
 
 
-@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("where", ["host", "host_gpu", "device"])
 def test_dropin_under_ccl_env_matches_reference_code(where, impl_env):
     """ccl_comp_reduce with the impl chosen by CCL_BF16 / CCL_FP16: every
-    2-input case, host (pageable) and device buffers."""
+    2-input case, on host (pageable) buffers — the dispatcher's CPU path, and
+    the GPU with that path off — and on device buffers."""
     import torch
+    impl_env("CCL_COMP_HOST_MAX_BYTES", "0" if where == "host_gpu" else str(32 << 20))
     for c in refvec.reduce_cases():
         impl_env(*ENV_NAME[(c["dtype"], c["impl"])])
-        if where == "host":
+        if where.startswith("host"):
             a, b = c["a"].copy(), c["b"].copy()
             comp.comp_reduce(a.ctypes.data, c["count"], b.ctypes.data, comp.datatype(c["dtype"]),
                              comp.reduction(c["op"]))

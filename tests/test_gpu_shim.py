@@ -21,6 +21,23 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
+def _gpu_dispatch():
+    """These tests drive the GPU paths (bounce buffers, staging, zero-copy) on
+    host buffers too, so the dispatcher's CPU path for small host buckets is
+    off here (CCL_COMP_HOST_MAX_BYTES=0, inherited by child processes);
+    tests/test_host_reduce.py and tests/test_gpu_dispatch.py cover it."""
+    saved = os.environ.get("CCL_COMP_HOST_MAX_BYTES")
+    os.environ["CCL_COMP_HOST_MAX_BYTES"] = "0"
+    comp.env_reload()
+    yield
+    if saved is None:
+        os.environ.pop("CCL_COMP_HOST_MAX_BYTES", None)
+    else:
+        os.environ["CCL_COMP_HOST_MAX_BYTES"] = saved
+    comp.env_reload()
+
+
+@pytest.fixture(autouse=True)
 def _reset_env():
     saved = {k: os.environ.get(k) for k in ("CCL_BF16", "CCL_FP16")}
     yield

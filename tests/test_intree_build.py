@@ -82,14 +82,20 @@ def objs(tmp_path_factory):
     jobs = {name: (REF / rel, d / f"{name}.o", ()) for name, rel in {**REPLACED, **KEPT, **OTHER}.items()}
     jobs["ours"] = (ROOT / "oneccl_amd" / "csrc" / "comp.cpp", d / "ours.o",
                     ("-DMI_ONECCL_TREE", f"-I{ROOT / 'include'}"))
+    # the host reduce, with the per-source ISA options of INTEGRATION.md §2a
+    jobs["ours_host"] = (ROOT / "oneccl_amd" / "csrc" / "host_reduce.cpp", d / "ours_host.o",
+                         ("-mavx2", "-mf16c", "-mfma"))
+    jobs["ours_host512"] = (ROOT / "oneccl_amd" / "csrc" / "host_reduce_avx512.cpp", d / "ours_host512.o",
+                            ("-mavx2", "-mf16c", "-mfma", "-mavx512f", "-mavx512bw", "-mavx512vl", "-mavx512bf16"))
     with ThreadPoolExecutor(4) as ex:
         res = dict(zip(jobs, ex.map(lambda j: _compile(*j), jobs.values())))
     return {name: (jobs[name][1], r) for name, r in res.items()}
 
 
 def test_intree_translation_unit_compiles_with_reference_flags(objs):
-    out, r = objs["ours"]
-    assert r.returncode == 0, r.stderr[-3000:]
+    for name in ("ours", "ours_host", "ours_host512"):
+        out, r = objs[name]
+        assert r.returncode == 0, (name, r.stderr[-3000:])
     for name in (*REPLACED, *KEPT, *OTHER):  # the same command builds the reference's own sources
         assert objs[name][1].returncode == 0, (name, objs[name][1].stderr[-2000:])
 
@@ -103,7 +109,8 @@ def test_intree_object_defines_every_replaced_symbol(objs):
 
 
 def test_intree_object_needs_nothing_the_tree_does_not_provide(objs):
-    need = _undefs(objs["ours"][0])
+    ours = ("ours", "ours_host", "ours_host512")
+    need = set().union(*(_undefs(objs[n][0]) for n in ours)) - set().union(*(_global_defs(objs[n][0]) for n in ours))
     provided = set().union(*(_undefs(objs[n][0]) for n in REPLACED))  # already resolved inside libccl
     provided |= _global_defs(objs["datatype"][0])  # ccl_datatype's constructor
     provided |= _dyn_defs(str(ROOT / "oneccl_amd" / "lib" / "libmi_reduce.so"))
@@ -111,6 +118,9 @@ def test_intree_object_needs_nothing_the_tree_does_not_provide(objs):
                 "/lib/x86_64-linux-gnu/libgcc_s.so.1", "/lib/x86_64-linux-gnu/libm.so.6"):
         if Path(lib).exists():
             provided |= _dyn_defs(lib)
+    libgcc = subprocess.run(["g++", "-print-libgcc-file-name"], capture_output=True, text=True).stdout.strip()
+    if libgcc and Path(libgcc).exists():  # the compiler's static runtime (__builtin_cpu_supports' data)
+        provided |= {s for t, s in _nm(Path(libgcc), "--defined-only") if t in "TBDRC"}
     provided |= {"_GLOBAL_OFFSET_TABLE_", "__dso_handle"}
     missing = sorted(need - provided)
     assert not missing, missing

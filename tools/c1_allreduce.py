@@ -63,12 +63,14 @@ def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs, fused=None):
 
 def worker(rank, world, port, count, iters, mode, q, fused_call=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if mode == "dropin-gpu":  # the drop-in with its CPU path off: every reduce on the GPU
+        os.environ["CCL_COMP_HOST_MAX_BYTES"] = "0"
     import numpy as np
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if mode == "dropin":
+        if mode in ("dropin", "dropin-gpu"):
             from oneccl_amd import comp
 
             def reduce2(inp, inout):
@@ -85,7 +87,7 @@ def worker(rank, world, port, count, iters, mode, q, fused_call=False):
         recv = {p: recv_all[p * per:(p + 1) * per] for p in range(world)}
         fused = None
         if fused_call:
-            if mode == "dropin":
+            if mode in ("dropin", "dropin-gpu"):
                 from oneccl_amd import comp
 
                 def fused(r, own):
@@ -145,7 +147,9 @@ if __name__ == "__main__":
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--count", type=int, default=262144)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--reduce", default="dropin", choices=["dropin", "oracle"])
+    ap.add_argument("--reduce", default="dropin", choices=["dropin", "dropin-gpu", "oracle"],
+                    help="dropin: the shim with its default dispatch (small host chunks on the CPU); "
+                         "dropin-gpu: the shim with every reduce on the GPU; oracle: the CPU restatement")
     ap.add_argument("--fused", action="store_true", help="one ccl_comp_batch_reduce per rank")
     a = ap.parse_args()
     print(json.dumps(run(a.ranks, a.count, a.iters, a.reduce, a.fused)), flush=True)

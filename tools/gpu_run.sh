@@ -54,11 +54,15 @@ for step in "$@"; do
         warm)
             run warm 300 python tools/warm_probe.py ;;
         c1)
-            run c1_dropin 300 python tools/c1_allreduce.py --reduce dropin &&
-            run c1_oracle 300 python tools/c1_allreduce.py --reduce oracle &&
-            run c1_dropin_p4 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 &&
-            run c1_dropin_p4_fused 300 python tools/c1_allreduce.py --reduce dropin --ranks 4 --fused &&
-            run c1_oracle_p4 300 python tools/c1_allreduce.py --reduce oracle --ranks 4 ;;
+            for P in 2 4; do
+                for mode in dropin dropin-gpu oracle; do
+                    run "c1_${mode}_p$P" 300 python tools/c1_allreduce.py --reduce $mode --ranks $P --iters 200 &&
+                    run "c1_${mode}_p${P}_fused" 300 python tools/c1_allreduce.py --reduce $mode --ranks $P \
+                        --iters 200 --fused
+                done
+            done ;;
+        dispatch)
+            run dispatch 600 python tools/dispatch_sweep.py --max-mib ${DISPATCH_MAX_MIB:-512} ;;
         dist2)
             run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo &&
