@@ -127,8 +127,25 @@ def cpu_baseline(cfg, seconds):
     (b1, m1, r1) = res[1]
     nt = max(res)
     (bn, mn, rn) = res[nt]
+    # sanity probe, independent of the oracle: one core's memcpy bandwidth
+    # over the same footprint (numpy's copy is a single-threaded memcpy)
+    src = np.ones(bucket // 8, np.float64)
+    dst = np.empty_like(src)
+    np.copyto(dst, src)
+    ct = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        np.copyto(dst, src)
+        ct.append(time.perf_counter() - t0)
+    copy_gbps = 2 * src.nbytes / min(ct) / 1e9
+    del src, dst
     return {
         "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "traffic_GBps_1core": round(b1 * GiB * (k + 1) / 1e9, 1),
+        "copy_probe_GBps_1core": round(copy_gbps, 1),
+        "traffic_note": f"the 1-core rate moves (k+1) = {k + 1} bucket-sizes of DRAM traffic per reduce; "
+                        "copy_probe = 2 x bytes / time of one single-threaded memcpy of the bucket (read + "
+                        "write), measured in the same run as an independent ceiling for one core",
         "sample": f"oracle/comp_oracle.c (CPU restatement of src/comp CCL_REDUCE loop, gcc -O3) on the same "
                   f"{bucket // (1 << 20)} MiB bucket x {k}-input, best of {r1} reps (median {m1:.2f} GiB/s); "
                   f"1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
@@ -151,6 +168,73 @@ def plan(n_total, es, rank, world, scaling):
     lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
     _lib.check(_lib.mi().mi_shard_range(n_total, rank, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
     return hi.value - lo.value, lo.value, n_total * es
+
+
+def timed_steps(step, steps, warmup, stream, world):
+    """W untimed steps, then exactly K steps bracketed by a barrier and a
+    device synchronize on both sides; every launch between a HIP event pair
+    on the launch stream.  Returns (wall s, mean launch ms, launch ms list)."""
+    import torch
+    import torch.distributed as dist
+
+    from oneccl_amd import _lib
+    for _ in range(warmup):
+        _lib.check(step(), "mi_reduce")
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        rc = step()
+        ev[i][1].record(stream)
+        if rc:
+            _lib.check(rc, "mi_reduce")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return elapsed, statistics.mean(kern_ms), kern_ms
+
+
+def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None):
+    """One bucket of n_total elements split by element range over the ranks
+    (mi_shard_range, 256-element aligned; BASELINE configs[3] as written):
+    this rank reduces its shard of all k inputs.  `ins` (optional) holds
+    device buffers at least a shard long to reuse.  value = the whole
+    bucket / max-over-ranks wall time."""
+    import torch
+    n, _, total_bytes = plan(n_total, es, rank, world, "strong")
+    tdt = torch_dtype(dt)
+    if ins is None:
+        ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+        for j, t in enumerate(ins):
+            fill(t, 0xA0 + j + 7919 * rank)
+    from oneccl_amd import _lib
+    arr = _lib.void_ptr_array([t.data_ptr() for t in ins[:k]])
+    sh = stream.cuda_stream
+
+    def step():
+        if k == 2:
+            return m.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)
+        return m.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
+
+    elapsed, avg_ms, _ = timed_steps(step, steps, warmup, stream, world)
+    elapsed, avg_ms_max = max_over_ranks([elapsed, avg_ms], world, coll_dev)
+    algo = (k + 1) * n * es
+    return {"value": round(total_bytes * steps / elapsed / GiB, 2), "unit": "GiB/s", "inputs": k,
+            "bucket_bytes_total": total_bytes, "shard_bytes_per_gpu": n * es,
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "avg_kernel_ms_max_rank": round(avg_ms_max, 5),
+            "aggregate_roofline": {"achieved": round((k + 1) * total_bytes / (avg_ms_max / 1e3) / 1e9, 1),
+                                   "peak": HBM_PEAK_GBPS * world,
+                                   "frac": round((k + 1) * total_bytes / (avg_ms_max / 1e3) / 1e9 /
+                                                 (HBM_PEAK_GBPS * world), 4)},
+            "per_rank_launch_bytes": algo,
+            "scaling": "strong", "note": "one bucket split by element range over the ranks, no collective"}
 
 
 def max_over_ranks(vals, world, device):
@@ -185,6 +269,7 @@ def main():
         else:
             dist.init_process_group("gloo")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    pg_world = dist.get_world_size() if world > 1 else 1  # the ranks the process group saw
 
     cfg = CONFIGS[args.config]
     desc, dt, es, op, k, bucket, flags = cfg
@@ -217,28 +302,7 @@ def main():
         expect = torch.tensor(a0, dtype=torch.float32) + torch.tensor(b0, dtype=torch.float32)
         assert ins[0][123].item() == expect.item(), "probe mismatch"
 
-    for _ in range(args.warmup):
-        _lib.check(step(), "mi_reduce")
-    torch.cuda.synchronize()
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        rc = step()
-        ev[i][1].record(stream)
-        if rc:
-            _lib.check(rc, "mi_reduce")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    avg_kern_ms = statistics.mean(kern_ms)
-
+    elapsed, avg_kern_ms, kern_ms = timed_steps(step, args.steps, args.warmup, stream, world)
     elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, coll_dev)
 
     units_per_rank = n * es  # bucket bytes this rank reduced per step
@@ -273,14 +337,27 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, args.cpu_seconds)
 
-    traffic = pmc_traffic(args.config)
+    # BASELINE configs[3] as written at N > 1: one 1 GiB bucket split over the
+    # GPUs, beside the weak-scaling `value` (each GPU its own 1 GiB bucket):
+    # the 2-input headline bucket and the 8-input fan-in
+    strong = None
+    if world > 1 and args.config == "c2":
+        strong = {"c2": strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, args.steps,
+                                     args.warmup, coll_dev, ins=ins)}
+        del ins
+        torch.cuda.empty_cache()
+        strong["c4_fanin8"] = strong_split(m, 9, 4, 0, 8, 0, GiB // 4, rank, world, stream, args.steps,
+                                           args.warmup, coll_dev)
+        torch.cuda.empty_cache()
+
+    traffic = pmc_traffic(args.config, traffic_per_launch)
     if rank == 0:
         out = {
             "metric": "GiB/s device-resident fp32 sum-reduce of 1 GiB bucket; 1/2/4/8 MI355X"
             if args.config == "c2" else f"GiB/s device-resident {args.config} bucket reduce",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": pg_world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -296,6 +373,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                         "traffic_ratio_to_algorithmic": traffic.get("ratio") if traffic else None,
                          "algorithmic_bytes_per_launch": traffic_per_launch,
                          "avg_kernel_ms": round(avg_kern_ms, 5), "avg_kernel_ms_max_rank": round(avg_kern_ms_max, 5),
                          "kernel_ms_min": round(min(kern_ms), 5),
@@ -306,6 +384,8 @@ def main():
                          "traffic_source": traffic.get("source") if traffic else None},
             "cpu_baseline": cpu,
         }
+        if strong:
+            out["strong_split"] = strong
         if dropin:
             out["dropin_sync"] = dropin
         if host_leg:
@@ -399,16 +479,28 @@ def host_shard_probe(n, dt, es, op, flags):
                       "bucket_bytes": nn * es, "entry": "mi_reduce_multi_sync_sharded"}), flush=True)
 
 
-def pmc_traffic(config):
+def pmc_traffic(config, algo_bytes):
     """HBM bytes per launch from the committed rocprofv3 PMC pass
-    (profiles/*pmc*.json, produced by tools/pmc_traffic.py), if present."""
+    (profiles/*pmc*.json, produced by tools/pmc_traffic.py), if present.  The
+    pass is a 1-GPU full-bucket run; a launch of another size (a strong-
+    scaling shard) gets the measured ratio to algorithmic bytes applied to
+    its own algorithmic bytes."""
     for p in sorted((ROOT / "profiles").glob("*pmc*.json")):
         try:
             d = json.loads(p.read_text())
         except (OSError, ValueError):
             continue
-        if isinstance(d.get(config), dict) and "hbm_bytes_per_launch" in d[config]:
-            return {"bytes_per_launch": d[config]["hbm_bytes_per_launch"], "source": str(p.relative_to(ROOT))}
+        e = d.get(config)
+        if not isinstance(e, dict) or "hbm_bytes_per_launch" not in e:
+            continue
+        pmc_algo = e.get("algorithmic_bytes_per_launch")
+        if not pmc_algo:
+            continue
+        ratio = e["hbm_bytes_per_launch"] / pmc_algo
+        src = str(p.relative_to(ROOT))
+        if pmc_algo != algo_bytes:
+            src += f" (ratio {ratio:.6f} of a {pmc_algo}-B launch, applied to this {algo_bytes}-B launch)"
+        return {"bytes_per_launch": int(round(ratio * algo_bytes)), "ratio": round(ratio, 6), "source": src}
     return None
 
 

@@ -109,6 +109,14 @@ def build_fan_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_burst_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "burst_sweep"
+    src = ROOT / "tools" / "burst_sweep.hip"
+    if src.exists() and (force or _stale(out, [src, CSRC / "reduce_kernels.hpp"])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
 def build_latency(force: bool = False) -> Path:
     out = ROOT / "tools" / "latency"
     src = ROOT / "tools" / "latency.hip"
@@ -189,6 +197,7 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_sweep()
     build_policy_sweep()
     build_fan_sweep()
+    build_burst_sweep()
     build_latency()
     if asan:
         build_asan(force)

@@ -54,7 +54,8 @@ static int mi_comp_device() {
     }();
     return dev;
 }
-static size_t mi_host_max_bytes();
+struct HostMax;
+static HostMax mi_host_max();
 #else
 #include "../../include/mi_ccl_comp.h"
 #include "ccl_mirror.hpp"
@@ -87,22 +88,38 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
     std::make_pair(ccl_fp16_f16c, "f16c"), std::make_pair(ccl_fp16_avx512f, "avx512f"),
     std::make_pair(ccl_fp16_avx512fp16, "avx512fp16")};
 
-// CCL_COMP_HOST_MAX_BYTES=<n>: a reduce whose operands are all host memory
-// (pageable or pinned) and whose bucket is at most n bytes runs on the
-// calling thread's CPU (host_reduce.cpp), as the reference runs every reduce;
+// A reduce whose operands are all host memory runs on the calling thread's
+// CPU (host_reduce.cpp), as the reference runs every reduce, when its bucket
+// is at most
+//   CCL_COMP_HOST_MAX_BYTES         bytes, if any operand is pageable memory
+//                                   (the GPU would stage it), default 64 MiB;
+//   CCL_COMP_HOST_MAX_PINNED_BYTES  bytes, if all are pinned (the GPU reads
+//                                   them in place over PCIe), default 16 MiB;
 // larger ones and all device operands run on the GPU.  0 = always the GPU.
-// The default is the crossover measured on MI355X.
-static const size_t kHostMaxBytesDefault = 32ull << 20;
+// The defaults are the crossovers measured on MI355X (EPYC 9575F host):
+// pageable, one core 23 GiB/s vs staged GPU 18 GiB/s at 64 MiB, even at
+// 128 MiB; pinned, 709 vs 757 us at 16 MiB, GPU ahead from 32 MiB
+// (profiles/round2_dispatch/).
+static const size_t kHostMaxPageableDefault = 64ull << 20;
+static const size_t kHostMaxPinnedDefault = 16ull << 20;
 
-static size_t parse_host_max() {
-    if (!mi_host_supported()) return 0;  // no AVX2/F16C: the GPU takes everything
+struct HostMax {
+    size_t pageable = 0, pinned = 0;
+};
+
+static HostMax parse_host_max() {
+    HostMax m;
+    if (!mi_host_supported()) return m;  // no AVX2/F16C: the GPU takes everything
     const char* v = getenv("CCL_COMP_HOST_MAX_BYTES");
-    return v ? (size_t)strtoull(v, nullptr, 0) : kHostMaxBytesDefault;
+    const char* p = getenv("CCL_COMP_HOST_MAX_PINNED_BYTES");
+    m.pageable = v ? (size_t)strtoull(v, nullptr, 0) : kHostMaxPageableDefault;
+    m.pinned = p ? (size_t)strtoull(p, nullptr, 0) : std::min(kHostMaxPinnedDefault, m.pageable);
+    return m;
 }
 
 #ifdef MI_ONECCL_TREE
-static size_t mi_host_max_bytes() {
-    static const size_t m = parse_host_max();  // read once, like oneCCL's env
+static HostMax mi_host_max() {
+    static const HostMax m = parse_host_max();  // read once, like oneCCL's env
     return m;
 }
 #endif
@@ -119,7 +136,7 @@ struct MiEnv {
     ccl_bf16_impl_type bf16 = ccl_bf16_scalar;
     ccl_fp16_impl_type fp16 = ccl_fp16_no_compiler_support;
     int device = -1;  // CCL_COMP_HIP_DEVICE
-    size_t host_max = 0;  // CCL_COMP_HOST_MAX_BYTES
+    HostMax host_max;  // CCL_COMP_HOST_MAX_BYTES, CCL_COMP_HOST_MAX_PINNED_BYTES
 };
 
 std::mutex g_env_mu;
@@ -203,7 +220,7 @@ const MiEnv& env() {
 static ccl_bf16_impl_type mi_bf16_impl() { return env().bf16; }
 static ccl_fp16_impl_type mi_fp16_impl() { return env().fp16; }
 static int mi_comp_device() { return env().device; }
-static size_t mi_host_max_bytes() { return env().host_max; }
+static HostMax mi_host_max() { return env().host_max; }
 #endif  // !MI_ONECCL_TREE
 
 // ---------------------------------------------------------------------------
@@ -356,20 +373,31 @@ void shard_env_reload() {  // standalone only: oneCCL's env is read once, at ini
 }
 #endif
 
-// Are all these operands host memory (pageable or pinned)?
-bool all_host(const void* const* ptrs, int n, const void* out) {
-    if (is_device_ptr(out)) return false;
-    for (int i = 0; i < n; i++)
-        if (is_device_ptr(ptrs[i])) return false;
-    return true;
+// Host kind of a set of operands: 0 = some operand is device memory,
+// 1 = all pinned host memory, 2 = host memory, some of it pageable.
+int host_kind(const void* const* ptrs, int n, const void* out) {
+    int dev = -1, kind = mi_pointer_kind(out, &dev);
+    if (kind == 0) return 0;
+    for (int i = 0; i < n; i++) {
+        const int k = mi_pointer_kind(ptrs[i], &dev);
+        if (k == 0) return 0;
+        kind = std::max(kind, k);
+    }
+    return kind;
 }
 
-// The dispatcher: host-resident buckets up to CCL_COMP_HOST_MAX_BYTES stay on
-// the calling thread's CPU: below the crossover a GPU
-// round trip costs more than the reduce.
+bool all_host(const void* const* ptrs, int n, const void* out) { return host_kind(ptrs, n, out) != 0; }
+
+// The dispatcher: host-resident buckets up to the crossover stay on the
+// calling thread's CPU: below it a GPU round trip
+// costs more than the reduce.
 bool host_path(const void* const* ins, int k, const void* out, size_t bytes) {
-    const size_t m = mi_host_max_bytes();
-    return m > 0 && bytes <= m && all_host(ins, k, out);
+    const HostMax m = mi_host_max();
+    if (bytes > std::max(m.pageable, m.pinned)) return false;  // GPU whatever the kinds: skip classifying
+    const int kind = host_kind(ins, k, out);
+    if (kind == 0) return false;
+    const size_t lim = kind == 1 ? m.pinned : m.pageable;
+    return lim > 0 && bytes <= lim;
 }
 
 // the host path runs after this thread's outstanding asynchronous requests,
@@ -430,7 +458,7 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
     if (!in_buf) MI_CCL_THROW("in_buf is null");
     if (!out_buf) MI_CCL_THROW("out_buf is null");
     const void* src[1] = {in_buf};
-    if (mi_host_max_bytes() > 0 && all_host(src, 1, out_buf)) {  // host to host: a memcpy, as the reference
+    if (mi_host_max().pageable > 0 && all_host(src, 1, out_buf)) {  // host to host: a memcpy, as the reference
         check(mi_thread_sync(), "mi_thread_sync");
         memcpy(out_buf, in_buf, bytes);
         return ccl::status::success;

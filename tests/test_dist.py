@@ -75,3 +75,60 @@ def test_two_rank_gloo_plan_and_timing(scaling):
         oracle.comp_reduce(a, b, 9, 0)
         whole = np.concatenate([p for _, p in sorted(res[0][5], key=lambda x: x[0])])
         assert whole.tobytes() == b.tobytes()
+
+
+def _c4_worker(rank, world, port, q):
+    """BASELINE configs[3] as written: one 8-input fan-in bucket split by
+    element range over the ranks (bench.strong_split's plan)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_total, k = 300_017, 8
+        n, first, total = bench.plan(n_total, 4, rank, world, "strong")
+        rng = np.random.default_rng(11)
+        ins = [rng.standard_normal(n_total).astype(np.float32) for _ in range(k)]
+        shard = oracle.fanin([np.ascontiguousarray(x[first:first + n]) for x in ins], 9, 0)
+        parts = [None] * world
+        dist.all_gather_object(parts, (first, shard))
+        q.put((rank, n, total, parts))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_c4_strong_split_composes():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle
+    n_total = 300_017
+    assert sum(r[1] for r in res) == n_total and all(r[2] == n_total * 4 for r in res)
+    rng = np.random.default_rng(11)
+    ins = [rng.standard_normal(n_total).astype(np.float32) for _ in range(8)]
+    whole = np.concatenate([p for _, p in sorted(res[0][3], key=lambda x: x[0])])
+    assert whole.tobytes() == oracle.fanin(ins, 9, 0).tobytes()
+
+
+def test_pmc_traffic_scales_to_the_launch():
+    """roofline.traffic for a launch of another size (a strong-scaling
+    shard) is the measured PMC ratio applied to that launch's bytes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    full = bench.pmc_traffic("c2", 3 * (1 << 30))
+    if full is None:
+        pytest.skip("no committed PMC pass")
+    half = bench.pmc_traffic("c2", 3 * (1 << 29))
+    assert abs(half["bytes_per_launch"] * 2 - full["bytes_per_launch"]) <= 2
+    assert half["ratio"] == full["ratio"] and 0.99 < half["ratio"] < 1.01

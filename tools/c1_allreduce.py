@@ -48,17 +48,20 @@ def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs, fused=None):
             reqs.append(dist.irecv(recv_bufs[peer], peer))
     for r in reqs:
         r.wait()
+    t_red = time.perf_counter()
     if fused is not None:
         fused(rank, own)
     else:
         for peer in range(world):  # fold each peer's chunk into the owned chunk
             if peer != rank:
                 reduce2(recv_bufs[peer], own)
+    t_red = time.perf_counter() - t_red
     gathered = [torch.empty_like(own) for _ in range(world)]
     dist.all_gather(gathered, own)
     for i, g in enumerate(gathered):
         if i != rank:
             chunks[i].copy_(g)
+    return t_red
 
 
 def worker(rank, world, port, count, iters, mode, q, fused_call=False):
@@ -102,17 +105,19 @@ def worker(rank, world, port, count, iters, mode, q, fused_call=False):
                     oracle.batch_reduce(recv_all.numpy(), offs, per, own.numpy(), 9, 0, 0)
         buf = torch.empty(count, dtype=torch.float32)
         ok = True
-        times = []
+        times, red = [], []
         for it in range(iters + 3):
             buf.fill_(float(rank))
             dist.barrier()
             t0 = time.perf_counter()
-            nreduce_allreduce(buf, rank, world, reduce2, recv, fused)
+            tr = nreduce_allreduce(buf, rank, world, reduce2, recv, fused)
             dist.barrier()
             if it >= 3:
                 times.append(time.perf_counter() - t0)
+                red.append(tr)
             ok = ok and bool(torch.all(buf == (world - 1) * (world / 2)).item())
-        t = torch.tensor([min(times), float(np.median(times))], dtype=torch.float64)
+        t = torch.tensor([min(times), float(np.median(times)), min(red), float(np.median(red))],
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         q.put((rank, ok, t.tolist()))
     finally:
@@ -139,6 +144,8 @@ def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False):
             "iters": iters,
             "correct": all(r[1] for r in res) and all(p.exitcode == 0 for p in procs),
             "best_us": round(res[0][2][0] * 1e6, 1), "median_us": round(res[0][2][1] * 1e6, 1),
+            "reduce_best_us": round(res[0][2][2] * 1e6, 1), "reduce_median_us": round(res[0][2][3] * 1e6, 1),
+            "reduce_note": "time in the local reduce step (the src/comp calls) per allreduce, max over ranks",
             "reduce_calls_per_rank": 1 if fused_call else world - 1, "reduce_elems_per_call": count // world}
 
 

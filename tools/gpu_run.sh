@@ -41,6 +41,8 @@ for step in "$@"; do
             run sweep 300 ./tools/reduce_sweep 1024 ${SWEEP_ROUNDS:-3} 10 ;;
         fansweep)
             run fansweep 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
+        burst)
+            run burst 300 ./tools/burst_sweep 1024 ${SWEEP_ROUNDS:-3} 6 ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
         fanlayout)
