@@ -102,9 +102,16 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
 // (profiles/round2_dispatch/).
 static const size_t kHostMaxPageableDefault = 64ull << 20;
 static const size_t kHostMaxPinnedDefault = 16ull << 20;
+// Above the crossover a host bucket is split: the GPU reduces the tail while
+// the calling thread reduces a head of this share of the elements
+// (CCL_COMP_HOST_SHARE / CCL_COMP_HOST_SHARE_PINNED; 0 = the GPU alone).
+// Defaults from the measured one-core and GPU rates.
+static const double kHostShareDefault = 0.45;
+static const double kHostSharePinnedDefault = 0.3;
 
 struct HostMax {
     size_t pageable = 0, pinned = 0;
+    double share = 0, share_pinned = 0;  // cooperative split, see coop_fold
 };
 
 static HostMax parse_host_max() {
@@ -114,6 +121,11 @@ static HostMax parse_host_max() {
     const char* p = getenv("CCL_COMP_HOST_MAX_PINNED_BYTES");
     m.pageable = v ? (size_t)strtoull(v, nullptr, 0) : kHostMaxPageableDefault;
     m.pinned = p ? (size_t)strtoull(p, nullptr, 0) : std::min(kHostMaxPinnedDefault, m.pageable);
+    const char* sh = getenv("CCL_COMP_HOST_SHARE");
+    const char* shp = getenv("CCL_COMP_HOST_SHARE_PINNED");
+    m.share = std::min(0.95, std::max(0.0, sh ? atof(sh) : kHostShareDefault));
+    m.share_pinned = std::min(0.95, std::max(0.0, shp ? atof(shp) : kHostSharePinnedDefault));
+    if (m.pageable == 0) m.share = m.share_pinned = 0;  // "always the GPU"
     return m;
 }
 
@@ -410,9 +422,43 @@ int host_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
 // The synchronous fold every entry point ends in: the calling thread's CPU
 // for small host-resident buckets, otherwise one GPU, or, for host operands
 // under CCL_COMP_HIP_SHARD_DEVICES, several.
+// A host bucket above the crossover: the GPU takes the tail [s, count)
+// asynchronously (staged on this thread's worker, or the zero-copy kernel on
+// pinned memory) while the calling thread reduces the head [0, s) with the
+// host path; then it waits for the GPU part.  s is a multiple of 256
+// elements, so the bf16 keep-precision count % 16 tail stays in the last
+// part exactly as in the whole array.  Element-wise, so the bits are those of
+// either path alone.
+int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags, double share) {
+    const size_t es = mi_dtype_size(dt);
+    size_t s = (size_t)((double)count * share);
+    s -= s % 256;
+    if (s == 0 || s >= count) return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+    if (int rc = mi_thread_sync()) return rc;  // earlier requests of this thread first
+    const void* gins[MI_MAX_INPUTS];
+    for (int i = 0; i < k; i++) gins[i] = static_cast<const char*>(ins[i]) + s * es;
+    mi_request_t r = nullptr;
+    if (int rc = mi_reduce_start(gins, k, static_cast<char*>(out) + s * es, count - s, dt, op, flags,
+                                 mi_comp_device(), &r))
+        return rc;
+    const int hrc = mi_host_reduce(ins, k, out, s, dt, op, flags);
+    const int wrc = mi_wait(r);
+    (void)mi_request_free(r);
+    return wrc ? wrc : hrc;
+}
+
 int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags) {
-    if (host_path(ins, k, out, count * mi_dtype_size(dt))) return host_fold(ins, k, out, count, dt, op, flags);
+    const size_t bytes = count * mi_dtype_size(dt);
+    if (host_path(ins, k, out, bytes)) return host_fold(ins, k, out, count, dt, op, flags);
     const std::vector<int> devs = shard_devices();
+    if (devs.size() < 2) {
+        const HostMax m = mi_host_max();
+        if (m.share > 0 || m.share_pinned > 0) {
+            const int kind = host_kind(ins, k, out);
+            const double share = kind == 1 ? m.share_pinned : (kind == 2 ? m.share : 0.0);
+            if (share > 0) return coop_fold(ins, k, out, count, dt, op, flags, share);
+        }
+    }
     if (devs.size() >= 2) {
         bool host = !is_device_ptr(out);
         for (int i = 0; i < k && host; i++) host = !is_device_ptr(ins[i]);

@@ -19,19 +19,26 @@ from tests.util import BF16, FP32, assert_same, rand_array, to_dev, from_dev
 pytestmark = pytest.mark.gpu
 
 
+KNOBS = ("CCL_COMP_HOST_MAX_BYTES", "CCL_COMP_HOST_MAX_PINNED_BYTES", "CCL_COMP_HOST_SHARE",
+         "CCL_COMP_HOST_SHARE_PINNED")
+
+
 @pytest.fixture
 def threshold():
-    saved = os.environ.get("CCL_COMP_HOST_MAX_BYTES")
+    saved = {k: os.environ.get(k) for k in KNOBS}
 
-    def set_(v):
+    def set_(v, **kv):
         os.environ["CCL_COMP_HOST_MAX_BYTES"] = str(v)
+        for k, x in kv.items():
+            os.environ[k] = str(x)
         comp.env_reload()
 
     yield set_
-    if saved is None:
-        os.environ.pop("CCL_COMP_HOST_MAX_BYTES", None)
-    else:
-        os.environ["CCL_COMP_HOST_MAX_BYTES"] = saved
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     comp.env_reload()
 
 
@@ -104,3 +111,46 @@ def test_cpp_caller_with_default_dispatch():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin_caller: ok" in r.stdout
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+@pytest.mark.parametrize("dt,op", [(FP32, 0), (BF16, 3), (4, 1), (6, 2)])
+def test_cooperative_split_same_bits(kind, dt, op, threshold):
+    """Above the crossover a host bucket is split: the GPU reduces the tail
+    while the calling thread reduces the head.  Same bits as either path."""
+    import torch
+    threshold(1 << 20, CCL_COMP_HOST_SHARE=0.45, CCL_COMP_HOST_SHARE_PINNED=0.3)
+    b_impl, f_impl = comp.impl_types()
+    es = np.dtype(oracle.NP_DTYPE[dt]).itemsize
+    n = (24 << 20) // es + 13
+    a = rand_array(dt, n, seed=71 + op, op=op)
+    b = rand_array(dt, n, seed=72 + op, op=op)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, op, 8, int(b_impl), int(f_impl))
+    if kind == "pinned":
+        ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        tb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        comp.comp_reduce(ta.data_ptr(), n, tb.data_ptr(), comp.datatype(dt), comp.reduction(op))
+        got = tb.numpy().view(exp.dtype)
+    else:
+        comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype(dt), comp.reduction(op))
+        got = b
+    assert_same(got, exp, dt, f"{kind} split")
+
+
+@pytest.mark.parametrize("k", [4, 19])
+def test_cooperative_split_keep_precision_tail(k, threshold):
+    """bf16 keep-precision fan-in across the split: the count % 16 truncated
+    tail must land in the GPU's (last) part as in the whole array."""
+    threshold(1 << 20, CCL_COMP_HOST_SHARE=0.5)
+    b_impl, _ = comp.impl_types()
+    n = (3 << 20) + 11
+    ins = [rand_array(BF16, n, seed=500 + j, specials=False) for j in range(k)]
+    packed = np.concatenate(ins)
+    offsets = [j * n for j in range(k)]
+    exp = ins[0].copy()
+    oracle.batch_reduce(packed, offsets, n, exp, BF16, 0, 1, int(b_impl), 0)
+    got = ins[0].copy()
+    comp.comp_batch_reduce(packed.ctypes.data, offsets, n, got.ctypes.data, comp.datatype.bfloat16,
+                           comp.reduction.sum, 1)
+    assert_same(got, exp, BF16)

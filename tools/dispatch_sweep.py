@@ -21,6 +21,8 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 DT = {"f32": (9, 4), "bf16": (11, 2)}
+KNOBS = ("CCL_COMP_HOST_MAX_BYTES", "CCL_COMP_HOST_MAX_PINNED_BYTES", "CCL_COMP_HOST_SHARE",
+         "CCL_COMP_HOST_SHARE_PINNED")
 
 
 def best_us(fn, reps):
@@ -38,6 +40,8 @@ def main():
     ap.add_argument("--max-mib", type=int, default=512)
     ap.add_argument("--dtypes", default="f32,bf16")
     ap.add_argument("--kinds", default="pageable,pinned")
+    ap.add_argument("--shares", default="0.3,0.45,0.6")
+    ap.add_argument("--min-kib", type=int, default=4)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,7 +49,7 @@ def main():
     import oracle
     from oneccl_amd import comp
     sizes = []
-    s = 4 << 10
+    s = args.min_kib << 10
     while s <= args.max_mib << 20:
         sizes.append(s)
         s *= 2
@@ -66,16 +70,28 @@ def main():
                     b = np.ones(n, oracle.NP_DTYPE[dt])
                     pa, pb = a.ctypes.data, b.ctypes.data
                 row = {"dtype": dname, "kind": kind, "bytes": nbytes}
-                for mode, thr in (("cpu", str(1 << 40)), ("gpu", "0")):
-                    os.environ["CCL_COMP_HOST_MAX_BYTES"] = thr
+                modes = [("cpu", {"CCL_COMP_HOST_MAX_BYTES": str(1 << 40),
+                                  "CCL_COMP_HOST_MAX_PINNED_BYTES": str(1 << 40)}),
+                         ("gpu", {"CCL_COMP_HOST_MAX_BYTES": "0"}),
+                         ("default", {})]
+                if nbytes >= (32 << 20):  # the cooperative split (CPU head + GPU tail) at several shares
+                    for sh in args.shares.split(","):
+                        modes.append((f"coop{sh}", {"CCL_COMP_HOST_MAX_BYTES": str(1 << 20),
+                                                    "CCL_COMP_HOST_MAX_PINNED_BYTES": str(1 << 20),
+                                                    "CCL_COMP_HOST_SHARE": sh, "CCL_COMP_HOST_SHARE_PINNED": sh}))
+                for mode, envs in modes:
+                    for kk in KNOBS:
+                        os.environ.pop(kk, None)
+                    os.environ.update(envs)
                     comp.env_reload()
                     row[f"{mode}_us"], row[f"{mode}_median_us"] = best_us(
                         lambda: comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum), reps)
                 row["oracle_1t_us"], _ = best_us(lambda: oracle.comp_reduce(a, b, dt, 0), reps)
-                row["cpu_GiBps"] = round(nbytes / (row["cpu_us"] * 1e-6) / 2**30, 2)
-                row["gpu_GiBps"] = round(nbytes / (row["gpu_us"] * 1e-6) / 2**30, 2)
+                for mode, _ in modes:
+                    row[f"{mode}_GiBps"] = round(nbytes / (row[f"{mode}_us"] * 1e-6) / 2**30, 2)
                 print(json.dumps(row), flush=True)
-    os.environ.pop("CCL_COMP_HOST_MAX_BYTES", None)
+    for kk in KNOBS:
+        os.environ.pop(kk, None)
 
 
 if __name__ == "__main__":

@@ -65,6 +65,8 @@ for step in "$@"; do
             done ;;
         dispatch)
             run dispatch 600 python tools/dispatch_sweep.py --max-mib ${DISPATCH_MAX_MIB:-512} ;;
+        coop)  # the cooperative split above the crossover, shares swept
+            run coop 600 python tools/dispatch_sweep.py --min-kib 16384 --max-mib 1024 --shares 0.2,0.3,0.4,0.5,0.6 ;;
         dist2)
             run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo &&
