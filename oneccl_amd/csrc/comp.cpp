@@ -92,22 +92,22 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
 // CPU (host_reduce.cpp), as the reference runs every reduce, when its bucket
 // is at most
 //   CCL_COMP_HOST_MAX_BYTES         bytes, if any operand is pageable memory
-//                                   (the GPU would stage it), default 64 MiB;
+//                                   (the GPU would stage it), default 16 MiB;
 //   CCL_COMP_HOST_MAX_PINNED_BYTES  bytes, if all are pinned (the GPU reads
 //                                   them in place over PCIe), default 16 MiB;
-// larger ones and all device operands run on the GPU.  0 = always the GPU.
-// The defaults are the crossovers measured on MI355X (EPYC 9575F host):
-// pageable, one core 23 GiB/s vs staged GPU 18 GiB/s at 64 MiB, even at
-// 128 MiB; pinned, 709 vs 757 us at 16 MiB, GPU ahead from 32 MiB
-// (profiles/round2_dispatch/).
-static const size_t kHostMaxPageableDefault = 64ull << 20;
-static const size_t kHostMaxPinnedDefault = 16ull << 20;
-// Above the crossover a host bucket is split: the GPU reduces the tail while
+// larger host buckets are split between the GPU and the calling thread (see
+// coop_fold), and all device operands run on the GPU.  0 = always the GPU.
+// Above the threshold a host bucket is split: the GPU reduces the tail while
 // the calling thread reduces a head of this share of the elements
 // (CCL_COMP_HOST_SHARE / CCL_COMP_HOST_SHARE_PINNED; 0 = the GPU alone).
-// Defaults from the measured one-core and GPU rates.
+// The defaults come from the MI355X sweeps (EPYC 9575F host, DESIGN.md §6,
+// profiles/round2_dispatch/): below 16 MiB one core beats a GPU round trip
+// (4 KiB: 1.8 vs 16.7 us); from 32 MiB up the split at 0.45 moves 32-46
+// GiB/s against 21-23 for one core and 17-25 for the GPU alone.
+static const size_t kHostMaxPageableDefault = 16ull << 20;
+static const size_t kHostMaxPinnedDefault = 16ull << 20;
 static const double kHostShareDefault = 0.45;
-static const double kHostSharePinnedDefault = 0.3;
+static const double kHostSharePinnedDefault = 0.45;
 
 struct HostMax {
     size_t pageable = 0, pinned = 0;
