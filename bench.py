@@ -433,6 +433,29 @@ def host_resident_leg(m, dt, es, op, flags, n):
             m.mi_host_unregister(pb)
     m.mi_set_host_mode(0)
     res["register_ms_two_buffers"] = round(reg_s * 1e3, 2) if reg_s is not None else None
+    # the same bucket through oneCCL's entry point with the dispatcher's
+    # defaults: above its threshold the GPU reduces the tail while the
+    # calling thread reduces the head
+    from oneccl_amd import _lib
+    shim = _lib.shim()
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            pa, pb = a.data_ptr(), b.data_ptr()
+        else:
+            a = np.zeros(nbytes, np.uint8)
+            b = np.zeros(nbytes, np.uint8)
+            pa, pb = a.ctypes.data, b.ctypes.data
+        shim.mi_ccl_comp_reduce(pa, n, pb, None, dt, op)
+        times = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            rc = shim.mi_ccl_comp_reduce(pa, n, pb, None, dt, op)
+            times.append(time.perf_counter() - t0)
+            if rc:
+                return {"error": shim.mi_ccl_last_error().decode()}
+        res[f"dropin_{kind}"] = round(nbytes / GiB / min(times), 3)
     # several GPUs in one node: one pageable bucket split by element range over
     # all of them (mi_reduce_multi_sync_sharded), each shard over its own link.
     # Measured in a child process under a time limit: an extra leg never
@@ -450,7 +473,9 @@ def host_resident_leg(m, dt, es, op, flags, n):
             "bucket_bytes": nbytes, **res, "entry": "mi_reduce_sync",
             "modes": "pinned = zero-copy kernel on pinned host memory (default); pinned_staged = chunked "
                      "H2D/kernel/D2H over two streams; pageable = staged; pageable_registered = pageable buffers "
-                     "registered once with mi_host_register (cost in register_ms_two_buffers), then zero-copy"}
+                     "registered once with mi_host_register (cost in register_ms_two_buffers), then zero-copy; "
+                     "dropin_* = ccl_comp_reduce with the dispatcher's defaults (GPU tail + calling-thread "
+                     "CPU head above 16 MiB)"}
 
 
 def host_shard_probe(n, dt, es, op, flags):

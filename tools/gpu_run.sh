@@ -78,6 +78,8 @@ for step in "$@"; do
             run sizes 300 python tools/size_sweep.py --configs fp32-sum ;;
         misalign)
             run misalign 300 python tools/misalign_probe.py ;;
+        nanprobe)
+            run nanprobe 300 python tools/nan_probe.py ;;
         benchall)
             for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
