@@ -509,8 +509,8 @@ def pmc_traffic(config, algo_bytes):
     (profiles/*pmc*.json, produced by tools/pmc_traffic.py), if present.  The
     pass is a 1-GPU full-bucket run; a launch of another size (a strong-
     scaling shard) gets the measured ratio to algorithmic bytes applied to
-    its own algorithmic bytes."""
-    for p in sorted((ROOT / "profiles").glob("*pmc*.json")):
+    its own algorithmic bytes.  The newest round's pass wins."""
+    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
         try:
             d = json.loads(p.read_text())
         except (OSError, ValueError):
