@@ -395,30 +395,38 @@ def main():
         dist.destroy_process_group()
 
 
+def _host_pair(kind, nbytes):
+    """Two host buffers of `kind` ("pinned" or pageable), every byte 0x3F:
+    0.747 as fp32 (0.746 as bf16), so neither the CPU nor the GPU side meets
+    denormals.  (torch.empty's pinned pages held whatever was there before;
+    garbage fp32 denormals slowed the CPU head of the split 2.5x in one run.)"""
+    import numpy as np
+    import torch
+    if kind.startswith("pinned"):
+        a = torch.full((nbytes,), 0x3F, dtype=torch.uint8).pin_memory()
+        b = torch.full((nbytes,), 0x3F, dtype=torch.uint8).pin_memory()
+        return a, b, a.data_ptr(), b.data_ptr()
+    a = np.full(nbytes, 0x3F, np.uint8)
+    b = np.full(nbytes, 0x3F, np.uint8)
+    return a, b, a.ctypes.data, b.ctypes.data
+
+
 def host_resident_leg(m, dt, es, op, flags, n):
     """The path as oneCCL runs it (host staging buffers in, host result out):
     mi_reduce_sync with pinned and with pageable host buffers.  Reported
     beside `value`, never as it (PCIe-inclusive rate)."""
-    import numpy as np
     import torch
     res = {}
     nbytes = n * es
     reg_s = None
     for kind in ("pinned", "pinned_staged", "pageable", "pageable_registered"):
         m.mi_set_host_mode(1 if kind == "pinned_staged" else 0)
-        if kind.startswith("pinned"):
-            a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-            b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-            pa, pb = a.data_ptr(), b.data_ptr()
-        else:
-            a = np.zeros(nbytes, np.uint8)
-            b = np.zeros(nbytes, np.uint8)
-            pa, pb = a.ctypes.data, b.ctypes.data
-            if kind == "pageable_registered":  # what oneCCL's buffer cache would do once per buffer
-                t0 = time.perf_counter()
-                m.mi_host_register(pa, nbytes)
-                m.mi_host_register(pb, nbytes)
-                reg_s = time.perf_counter() - t0
+        a, b, pa, pb = _host_pair(kind, nbytes)
+        if kind == "pageable_registered":  # what oneCCL's buffer cache would do once per buffer
+            t0 = time.perf_counter()
+            m.mi_host_register(pa, nbytes)
+            m.mi_host_register(pb, nbytes)
+            reg_s = time.perf_counter() - t0
         m.mi_reduce_sync(pa, pb, n, dt, op, flags, -1)  # warm: staging buffers, page faults
         times = []
         for _ in range(5):
@@ -439,14 +447,7 @@ def host_resident_leg(m, dt, es, op, flags, n):
     from oneccl_amd import _lib
     shim = _lib.shim()
     for kind in ("pinned", "pageable"):
-        if kind == "pinned":
-            a = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-            b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-            pa, pb = a.data_ptr(), b.data_ptr()
-        else:
-            a = np.zeros(nbytes, np.uint8)
-            b = np.zeros(nbytes, np.uint8)
-            pa, pb = a.ctypes.data, b.ctypes.data
+        a, b, pa, pb = _host_pair(kind, nbytes)
         shim.mi_ccl_comp_reduce(pa, n, pb, None, dt, op)
         times = []
         for _ in range(5):

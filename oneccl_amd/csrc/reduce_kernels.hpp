@@ -99,25 +99,60 @@ __device__ __forceinline__ uint32_t f32_to_bf16_rne_int(float f) {
     return r;
 }
 
-// Same result via gfx950's v_cvt_pk_bf16_f32 (round to nearest even; a NaN
-// stays a NaN, payload not guaranteed — NaNs are compared NaN-agnostic):
-// flush denormals to signed zero first, in the integer domain so the
-// compiler cannot fold the flush into the conversion.  Two conversions pack
-// into one instruction; ~4 VALU ops per element.  Checked against the
-// oracle over all 2^32 fp32 inputs (tests/test_gpu_convert.py).
+__device__ __forceinline__ bool nan_bits(uint32_t u) { return (u & 0x7FFFFFFFu) > 0x7F800000u; }
+
+// Same result via gfx950's v_cvt_pk_bf16_f32 (round to nearest even): flush
+// denormals to signed zero first, in the integer domain so the compiler
+// cannot fold the flush into the conversion.  Two conversions pack into one
+// instruction; ~4 VALU ops per element.  X (exact NaN): a NaN takes
+// VCVTNEPS2BF16's quieted upper half explicitly — the hardware's NaN payload
+// is its own; the kernels run X only on rows holding an Inf or NaN
+// (fold_vec_x86).  Checked against the oracle over all 2^32 fp32 inputs, NaN
+// payloads included (tests/test_gpu_convert.py).
+template <bool X = true>
 __device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
     uint32_t u = __float_as_uint(f);
+    const uint32_t q = (u >> 16) | 0x40u;
     u = (u & 0x7F800000u) ? u : (u & 0x80000000u);
-    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)__uint_as_float(u));
+    const uint32_t r = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)__uint_as_float(u));
+    if constexpr (X) return nan_bits(u) ? q : r;
+    return r;
 }
 
-// VCVTPH2PS: exact widening (v_cvt_f32_f16; fp16 denormals are on by default).
+// VCVTPH2PS: exact widening (v_cvt_f32_f16; fp16 denormals are on by
+// default).  A signalling NaN may stay signalling here; every path that
+// stores the value quiets it the way x86 does (x86_nan_first, the narrowing
+// below, convert_elem), so stored bits match.
 __device__ __forceinline__ float fp16_to_f32(uint32_t h) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
 }
-// VCVTPS2PH imm8=0: round to nearest even (v_cvt_f16_f32, default RNE mode).
+// VCVTPS2PH imm8=0: round to nearest even (v_cvt_f16_f32, default RNE mode);
+// X: a NaN keeps its sign and top 10 payload bits, quieted (Intel SDM
+// VCVTPS2PH).
+template <bool X = true>
 __device__ __forceinline__ uint32_t f32_to_fp16_rne(float f) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+    const uint32_t u = __float_as_uint(f);
+    const uint32_t q = ((u >> 16) & 0x8000u) | 0x7E00u | ((u >> 13) & 0x3FFu);
+    const uint32_t r = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+    if constexpr (X) return nan_bits(u) ? q : r;
+    return r;
+}
+
+// x86 NaN propagation of ADDPS/MULPS(first, second) (Intel SDM vol. 1
+// §4.8.3.5): a NaN operand comes back quieted, the first source's when both
+// are; an invalid operation on numbers (inf - inf, 0 * inf) gives the default
+// NaN 0xFFC00000.  CDNA's ALUs choose their own NaN, so the low-precision
+// paths — whose reference is explicit AVX-512 code, _mm512_add_ps(in, inout)
+// (src/comp/bf16/bf16_intrisics.cpp:20-26, fp16_intrisics.hpp:58-63) — fix the
+// result up to those bits (oracle/comp_oracle.c x86_nan_first) on the rows
+// that need it (fold_vec_x86).
+__device__ __forceinline__ float x86_nan_first(float r, float first, float second) {
+    const uint32_t a = __float_as_uint(first), b = __float_as_uint(second);
+    uint32_t u = __float_as_uint(r);
+    u = nan_bits(u) ? 0xFFC00000u : u;
+    u = nan_bits(b) ? (b | 0x400000u) : u;
+    u = nan_bits(a) ? (a | 0x400000u) : u;
+    return __uint_as_float(u);
 }
 
 template <typename Tag>
@@ -131,15 +166,15 @@ __device__ __forceinline__ typename Tr<Tag>::C widen(typename Tr<Tag>::S s) {
 }
 
 // round a compute value to storage: per-step / final rounding
-template <typename Tag, unsigned V>
+template <typename Tag, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::S narrow(typename Tr<Tag>::C c) {
     if constexpr (std::is_same<Tag, bf16_tag>::value) {
         if constexpr (V & V_BF16_RNE)
-            return (uint16_t)f32_to_bf16_rne(c);
+            return (uint16_t)f32_to_bf16_rne<X>(c);
         else
             return (uint16_t)f32_to_bf16_trunc(c);
     } else if constexpr (std::is_same<Tag, fp16_tag>::value) {
-        return (uint16_t)f32_to_fp16_rne(c);
+        return (uint16_t)f32_to_fp16_rne<X>(c);
     } else {
         return c;
     }
@@ -177,25 +212,47 @@ __device__ __forceinline__ C apply(C in, C acc) {
     }
 }
 
-// one fold step in the variant's precision
-template <typename Tag, int OP, unsigned V>
+// one fold step in the variant's precision (X: x86 NaN bits, see above)
+template <typename Tag, int OP, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::C step(typename Tr<Tag>::C x, typename Tr<Tag>::C acc) {
     auto c = apply<OP, (V & V_INOUT_FIRST) != 0>(x, acc);
-    if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) c = widen<Tag>(narrow<Tag, V>(c));
+    if constexpr (X && Tr<Tag>::lp && (OP == OP_SUM || OP == OP_PROD)) c = x86_nan_first(c, x, acc);
+    if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) {
+        // Keep the fp32 result: left alone, the compiler turns
+        // fptrunc(fmul(fpext a, fpext b)) into a native v_pk_mul_f16, whose
+        // zero signs differed from VCVTPS2PH of the fp32 product on the
+        // GPU (fp16 prod chains gave +0 for -0; profiles/round2_nan/).
+        asm volatile("" : "+v"(c));
+        c = widen<Tag>(narrow<Tag, V, X>(c));
+    }
     return c;
 }
 
 // final rounding of the accumulator for element `idx`
-template <typename Tag, unsigned V>
+template <typename Tag, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::S finish(typename Tr<Tag>::C acc, uint64_t idx,
                                                       uint64_t trunc_from) {
     if constexpr (std::is_same<Tag, bf16_tag>::value && (V & V_TAIL_TRUNC)) {
         return (idx >= trunc_from) ? (uint16_t)f32_to_bf16_trunc(acc)
-                                   : (uint16_t)f32_to_bf16_rne(acc);
+                                   : (uint16_t)f32_to_bf16_rne<X>(acc);
     } else {
-        return narrow<Tag, V>(acc);
+        return narrow<Tag, V, X>(acc);
     }
 }
+
+// final store of a fold's accumulator.  In storage precision (bf16 without
+// V_ACC_FP32) every step has already rounded, so the accumulator holds a
+// bf16 value exactly and its upper half is the result: no second rounding
+// (it cost ~8 VALU ops per element pair on the C3 path).
+template <typename Tag, unsigned V, bool X = true>
+__device__ __forceinline__ typename Tr<Tag>::S finish_fold(typename Tr<Tag>::C acc, uint64_t idx,
+                                                           uint64_t trunc_from) {
+    if constexpr (std::is_same<Tag, bf16_tag>::value && !(V & V_ACC_FP32))
+        return (uint16_t)f32_to_bf16_trunc(acc);
+    else
+        return finish<Tag, V, X>(acc, idx, trunc_from);
+}
+
 
 template <int MEM>
 __device__ __forceinline__ u32x4 vload(const u32x4* p) {
@@ -216,6 +273,80 @@ template <typename S>
 struct alignas(16) Pack {
     S e[16 / sizeof(S)];
 };
+
+// ---------------------------------------------------------------------------
+// Fold of one 16-byte vector position across inputs x[0..k) (acc = x[0];
+// acc = op(x[i], acc); one final rounding) into the output vector.
+// fold_vec_x86 runs it without the NaN fix-ups, then screens the inputs for
+// an all-ones exponent (Inf or NaN) — 3 integer ops per dword, on the packed
+// words — and refolds the row with them only when one is present.  A
+// low-precision sum or product is NaN only from a NaN or Inf operand, except
+// a product chain whose partial product overflows to Inf and meets a zero
+// (K >= 3), which the screen of the result catches.  The fix-ups cost ~10
+// VALU ops per element; on every row they made C3 VALU-bound (28 % slower,
+// profiles/round2_nan/).
+// ---------------------------------------------------------------------------
+template <typename Tag>
+__device__ __forceinline__ uint32_t inf_nan_word(uint32_t w) {
+    // per 16-bit half (bf16, fp16) or per word (fp32): exponent field + one
+    // ulp of it carries into the top bit exactly when the field is all ones
+    if constexpr (std::is_same<Tag, bf16_tag>::value) return (w & 0x7F807F80u) + 0x00800080u;
+    else if constexpr (std::is_same<Tag, fp16_tag>::value) return (w & 0x7C007C00u) + 0x04000400u;
+    else return (w & 0x7F800000u) + 0x00800000u;
+}
+template <typename Tag>
+__device__ __forceinline__ uint32_t inf_nan_bits(u32x4 v) {
+    return inf_nan_word<Tag>(v.x) | inf_nan_word<Tag>(v.y) | inf_nan_word<Tag>(v.z) | inf_nan_word<Tag>(v.w);
+}
+template <typename Tag>
+__device__ __forceinline__ bool inf_nan_hit(uint32_t bits) {
+    return (bits & (sizeof(typename Tr<Tag>::S) == 2 ? 0x80008000u : 0x80000000u)) != 0u;
+}
+
+template <typename Tag, int OP, unsigned V, bool X, int KMAX>
+__device__ __forceinline__ u32x4 fold_vec(const u32x4 (&x)[KMAX], int k, uint64_t e0, uint64_t trunc_from) {
+    using S = typename Tr<Tag>::S;
+    using C = typename Tr<Tag>::C;
+    constexpr int N = 16 / sizeof(S);
+    C acc[N];
+    const Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0]);
+#pragma unroll
+    for (int e = 0; e < N; e++) acc[e] = widen<Tag>(p0.e[e]);
+#pragma unroll
+    for (int i = 1; i < KMAX; i++) {
+        if (i < k) {
+            const Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i]);
+#pragma unroll
+            for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V, X>(widen<Tag>(pi.e[e]), acc[e]);
+        }
+    }
+    Pack<S> pr;
+#pragma unroll
+    for (int e = 0; e < N; e++) pr.e[e] = finish_fold<Tag, V, X>(acc[e], e0 + e, trunc_from);
+    return __builtin_bit_cast(u32x4, pr);
+}
+
+// r = the fast fold of x; low precision: refold with the fix-ups when the
+// screen hits (a no-op for other types)
+template <typename Tag, int OP, unsigned V, int KMAX>
+__device__ __forceinline__ u32x4 x86_refold(u32x4 r, const u32x4 (&x)[KMAX], int k, uint64_t e0,
+                                            uint64_t trunc_from) {
+    if constexpr (Tr<Tag>::lp) {
+        uint32_t bits = inf_nan_bits<Tag>(x[0]);
+#pragma unroll
+        for (int i = 1; i < KMAX; i++)
+            if (i < k) bits |= inf_nan_bits<Tag>(x[i]);
+        if constexpr (OP == OP_PROD && KMAX > 2) bits |= inf_nan_bits<Tag>(r);
+        if (__builtin_expect(inf_nan_hit<Tag>(bits), 0)) r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
+    }
+    return r;
+}
+
+template <typename Tag, int OP, unsigned V, int KMAX>
+__device__ __forceinline__ u32x4 fold_vec_x86(const u32x4 (&x)[KMAX], int k, uint64_t e0, uint64_t trunc_from) {
+    return x86_refold<Tag, OP, V, KMAX>(fold_vec<Tag, OP, V, false, KMAX>(x, k, e0, trunc_from), x, k, e0,
+                                        trunc_from);
+}
 
 // ---------------------------------------------------------------------------
 // Packed 8- and 16-bit integer ops on whole dwords: acc' = op(in, acc) per
@@ -310,7 +441,7 @@ __device__ __forceinline__ void reduce_elem(const KArgs& a, int k, uint64_t idx)
     using C = typename Tr<Tag>::C;
     C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
     for (int i = 1; i < k; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
 }
 
 // One tile row: U vectors per lane at v0, v0+B, ...  GUARD = last tile.
@@ -389,7 +520,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
             Pack<S> p;
 #pragma unroll
             for (int e = 0; e < N; e++)
-                p.e[e] = finish<Tag, V>(acc[j][e], a.head + v * N + e, a.trunc_from);
+                p.e[e] = finish_fold<Tag, V>(acc[j][e], a.head + v * N + e, a.trunc_from);
             vstore<MEM>(po + v, __builtin_bit_cast(u32x4, p));
         }
     }
@@ -452,7 +583,7 @@ __device__ __forceinline__ void reduce2_elem(const R2Args& a, uint64_t idx) {
     using C = typename Tr<Tag>::C;
     C acc = widen<Tag>(static_cast<const S*>(a.acc)[idx]);
     acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in)[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
 }
 
 // One tile (block `blk` of the operand set `a`): the body of reduce2_kernel,
@@ -460,7 +591,6 @@ __device__ __forceinline__ void reduce2_elem(const R2Args& a, uint64_t idx) {
 template <typename Tag, int OP, unsigned V, int U, int B>
 __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
     using S = typename Tr<Tag>::S;
-    using C = typename Tr<Tag>::C;
     constexpr int N = 16 / sizeof(S);
     if (blk == 0) {
         if (threadIdx.x < a.head) reduce2_elem<Tag, OP, V>(a, threadIdx.x);
@@ -483,13 +613,8 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
     for (int j = 0; j < U; j++) {
         const uint64_t v = v0 + (uint64_t)j * B;
         if (full || v < a.nvec) {
-            Pack<S> px = __builtin_bit_cast(Pack<S>, x[j]), py = __builtin_bit_cast(Pack<S>, y[j]), pr;
-#pragma unroll
-            for (int e = 0; e < N; e++) {
-                const C r = step<Tag, OP, V>(widen<Tag>(py.e[e]), widen<Tag>(px.e[e]));
-                pr.e[e] = finish<Tag, V>(r, a.head + v * N + e, a.trunc_from);
-            }
-            vstore<3>(po + v, __builtin_bit_cast(u32x4, pr));
+            const u32x4 xs[2] = {x[j], y[j]};
+            vstore<3>(po + v, fold_vec_x86<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from));
         }
     }
 }
@@ -561,13 +686,12 @@ __device__ __forceinline__ void reducek_elem(const RKArgs& a, uint64_t idx) {
     C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
 #pragma unroll
     for (int i = 1; i < K; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
 }
 
 template <typename Tag, int OP, unsigned V, int K, int U, int B>
 __global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
     using S = typename Tr<Tag>::S;
-    using C = typename Tr<Tag>::C;
     constexpr int N = 16 / sizeof(S);
     if (blockIdx.x == 0) {
         if (threadIdx.x < a.head) reducek_elem<Tag, OP, V, K>(a, threadIdx.x);
@@ -589,20 +713,10 @@ __global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
     for (int j = 0; j < U; j++) {
         const uint64_t v = v0 + (uint64_t)j * B;
         if (full || v < a.nvec) {
-            C acc[N];
-            Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0][j]);
+            u32x4 xs[K];
 #pragma unroll
-            for (int e = 0; e < N; e++) acc[e] = widen<Tag>(p0.e[e]);
-#pragma unroll
-            for (int i = 1; i < K; i++) {
-                Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i][j]);
-#pragma unroll
-                for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V>(widen<Tag>(pi.e[e]), acc[e]);
-            }
-            Pack<S> pr;
-#pragma unroll
-            for (int e = 0; e < N; e++) pr.e[e] = finish<Tag, V>(acc[e], a.head + v * N + e, a.trunc_from);
-            vstore<3>(po + v, __builtin_bit_cast(u32x4, pr));
+            for (int i = 0; i < K; i++) xs[i] = x[i][j];
+            vstore<3>(po + v, fold_vec_x86<Tag, OP, V, K>(xs, K, a.head + v * N, a.trunc_from));
         }
     }
 }
@@ -629,7 +743,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, ui
 template <typename Tag, int OP, unsigned V, int B, int KMAX = kMaxInputs>
 __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
     using S = typename Tr<Tag>::S;
-    using C = typename Tr<Tag>::C;
     constexpr int N = 16 / sizeof(S);
     const int k = a.k;
     if (blockIdx.x == 0) {
@@ -663,6 +776,11 @@ __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
         return;
     }
+    // The fast fold is written out here rather than through fold_vec: with
+    // the runtime-k loop in a callee, the compiler kept the fp32 8-input
+    // form's x[] as an aggregate and spilled it to scratch (33 ms instead of
+    // 1.6 ms per GiB; tests/test_kernel_resources.py guards every kernel).
+    using C = typename Tr<Tag>::C;
     C acc[N];
     const Pack<S> p0 = __builtin_bit_cast(Pack<S>, x[0]);
 #pragma unroll
@@ -672,15 +790,16 @@ __global__ __launch_bounds__(B) void fan_kernel(KArgs a) {
         if (i < k) {
             const Pack<S> pi = __builtin_bit_cast(Pack<S>, x[i]);
 #pragma unroll
-            for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V>(widen<Tag>(pi.e[e]), acc[e]);
+            for (int e = 0; e < N; e++) acc[e] = step<Tag, OP, V, false>(widen<Tag>(pi.e[e]), acc[e]);
         }
     }
     Pack<S> pr;
     const uint64_t e0 = a.head + (t0 + threadIdx.x) * N;
 #pragma unroll
-    for (int e = 0; e < N; e++) pr.e[e] = finish<Tag, V>(acc[e], e0 + e, a.trunc_from);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pr), tile_rsrc(a.out, byte0, bytes), off, 0,
-                                           kAuxNT);
+    for (int e = 0; e < N; e++) pr.e[e] = finish_fold<Tag, V, false>(acc[e], e0 + e, a.trunc_from);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        x86_refold<Tag, OP, V, KMAX>(__builtin_bit_cast(u32x4, pr), x, k, e0, a.trunc_from),
+        tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
 }
 
 // The 2-input form of the same (R2Args: acc, in -> out).
@@ -698,16 +817,11 @@ __global__ __launch_bounds__(B) void reduce2b_kernel(R2Args a) {
     const uint32_t bytes = (uint32_t)(left < (uint64_t)B ? left : (uint64_t)B) * 16u;
     const uint64_t byte0 = (uint64_t)a.head * sizeof(S) + t0 * 16;
     const uint32_t off = threadIdx.x * 16u;
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.acc, byte0, bytes), off, 0, kAuxNT);
-    const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in, byte0, bytes), off, 0, kAuxNT);
-    const Pack<S> px = __builtin_bit_cast(Pack<S>, x), py = __builtin_bit_cast(Pack<S>, y);
-    Pack<S> pr;
+    const u32x4 xs[2] = {__builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.acc, byte0, bytes), off, 0, kAuxNT),
+                         __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in, byte0, bytes), off, 0, kAuxNT)};
     const uint64_t e0 = a.head + (t0 + threadIdx.x) * N;
-#pragma unroll
-    for (int e = 0; e < N; e++)
-        pr.e[e] = finish<Tag, V>(step<Tag, OP, V>(widen<Tag>(py.e[e]), widen<Tag>(px.e[e])), e0 + e, a.trunc_from);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pr), tile_rsrc(a.out, byte0, bytes), off, 0,
-                                           kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b128(fold_vec_x86<Tag, OP, V, 2>(xs, 2, e0, a.trunc_from),
+                                           tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
 }
 
 // ---------------------------------------------------------------------------
@@ -724,13 +838,26 @@ struct CArgs {
     int scalar_only;
 };
 
-template <typename ST, typename DT, unsigned V>
+// X: the reference's NaN bits (the vector body runs X only on groups whose
+// source holds an Inf or NaN, as fold_vec_x86 does)
+template <typename ST, typename DT, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<DT>::S convert_elem(typename Tr<ST>::S s, uint64_t idx, uint64_t trunc_from) {
-    const float f = widen<ST>(s);
+    float f = widen<ST>(s);
+    if constexpr (X && std::is_same<ST, fp16_tag>::value)  // VCVTPH2PS quiets a signalling NaN
+        f = nan_bits(__float_as_uint(f)) ? __uint_as_float(__float_as_uint(f) | 0x400000u) : f;
     if constexpr (std::is_same<DT, float>::value)
         return f;
     else
-        return finish<DT, V>(f, idx, trunc_from);
+        return finish<DT, V, X>(f, idx, trunc_from);
+}
+
+template <typename ST, typename DT, unsigned V, bool X, int SV, int DV>
+__device__ __forceinline__ void convert_group(const Pack<typename Tr<ST>::S> (&sp)[SV],
+                                              Pack<typename Tr<DT>::S> (&dp)[DV], uint64_t e0, uint64_t trunc_from) {
+    constexpr int SN = 16 / sizeof(typename Tr<ST>::S), DN = 16 / sizeof(typename Tr<DT>::S);
+#pragma unroll
+    for (int e = 0; e < 8; e++)
+        dp[e / DN].e[e % DN] = convert_elem<ST, DT, V, X>(sp[e / SN].e[e % SN], e0 + e, trunc_from);
 }
 
 // 8 elements per lane per group: fp32 side 2 x 16 B, 16-bit side 16 B.
@@ -756,10 +883,12 @@ __global__ __launch_bounds__(kBlock) void convert_kernel(CArgs a) {
 #pragma unroll
         for (int v = 0; v < SV; v++) sp[v] = __builtin_bit_cast(Pack<SS>, vload<3>(src + i * SV + v));
         Pack<DS> dp[DV];
+        convert_group<ST, DT, V, false>(sp, dp, a.head + i * 8, a.trunc_from);
+        if constexpr (!std::is_same<ST, bf16_tag>::value) {  // bf16 -> fp32 is a shift: bits exact as is
+            uint32_t bits = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            constexpr int SN = 16 / sizeof(SS), DN = 16 / sizeof(DS);
-            dp[e / DN].e[e % DN] = convert_elem<ST, DT, V>(sp[e / SN].e[e % SN], a.head + i * 8 + e, a.trunc_from);
+            for (int v = 0; v < SV; v++) bits |= inf_nan_bits<ST>(__builtin_bit_cast(u32x4, sp[v]));
+            if (__builtin_expect(inf_nan_hit<ST>(bits), 0)) convert_group<ST, DT, V, true>(sp, dp, a.head + i * 8, a.trunc_from);
         }
 #pragma unroll
         for (int v = 0; v < DV; v++) vstore<3>(dst + i * DV + v, __builtin_bit_cast(u32x4, dp[v]));

@@ -343,6 +343,12 @@ void orc_convert_fp32_to_fp16_arrays(const float* src, uint16_t* dst, size_t cou
     for (size_t i = 0; i < count; i++) dst[i] = orc_fp32_to_fp16_rne(src[i]);
 }
 
+/* ccl_convert_fp16_to_fp32 (fp16.cpp:59-61) applied over an array: VCVTPH2PS
+ * on every element (a signalling NaN comes back quiet). */
+void orc_convert_fp16_to_fp32_arrays(const uint16_t* src, float* dst, size_t count) {
+    for (size_t i = 0; i < count; i++) dst[i] = orc_fp16_to_fp32(src[i]);
+}
+
 void orc_convert_bf16_to_fp32_arrays(const uint16_t* src, float* dst, size_t count) {
     for (size_t i = 0; i < count; i++) dst[i] = orc_bf16_to_fp32(src[i]);
 }

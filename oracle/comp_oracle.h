@@ -59,6 +59,7 @@ void orc_convert_fp32_to_bf16_arrays(const float* fp32_buf, uint16_t* bf16_buf,
 void orc_convert_bf16_to_fp32_arrays(const uint16_t* bf16_buf, float* fp32_buf,
                                      size_t count);
 void orc_convert_fp32_to_fp16_arrays(const float* fp32_buf, uint16_t* fp16_buf, size_t count);
+void orc_convert_fp16_to_fp32_arrays(const uint16_t* fp16_buf, float* fp32_buf, size_t count);
 
 /* Scalar conversions (exposed for the unit tests). */
 float orc_bf16_to_fp32(uint16_t v);

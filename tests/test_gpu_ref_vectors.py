@@ -5,10 +5,11 @@ the C ABI with the flags of each impl, and through the drop-in shim with
 CCL_BF16 / CCL_FP16 selecting the impl, as oneCCL's env does
 (src/common/env/env.cpp:711-720).
 
-Bar: bit-exact, NaN payloads excepted (two NaNs compare equal, NaN-ness must
-match): the AVX-512 code returns the first NaN operand quieted and x86's
-default NaN 0xFFC00000, CDNA's ALUs their own (the oracle, which does match
-the payloads, is pinned to these vectors in tests/test_ref_vectors.py)."""
+Bar: bit-exact, NaN payloads included: the AVX-512 code returns the first NaN
+operand quieted and x86's default NaN 0xFFC00000, and the kernels restate
+that rule (reduce_kernels.hpp x86_nan_first and the NaN selects of the
+narrowing conversions) instead of taking CDNA's ALU NaNs.  The oracle is
+pinned to the same vectors in tests/test_ref_vectors.py."""
 from __future__ import annotations
 
 import os

@@ -43,6 +43,18 @@ for step in "$@"; do
             run fansweep 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
         burst)
             run burst 300 ./tools/burst_sweep 1024 ${SWEEP_ROUNDS:-3} 6 ;;
+        burstpmc)  # memory-side counters of every burst_sweep variant (tools/pmc_burst.py summarises)
+            i=0
+            for p in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum" \
+                     "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_CYCLE_sum"; do
+                d="$GRAFT_REPO_ROOT/$OUT/pmcburst_$i"
+                (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $p --output-format csv -d "$d" -o burst -- \
+                    "$GRAFT_REPO_ROOT/tools/burst_sweep" 1024 1 2 > "$d.out" 2> "$d.err")
+                rc=$?; echo "=== pmcburst $i rc=$rc" | tee -a "$OUT/steps.log"
+                [ $rc -eq 0 ] || exit $rc
+                i=$((i+1))
+            done
+            python tools/pmc_burst.py "$OUT/pmc_burst.json" "$OUT/pmcburst" > "$OUT/pmc_burst.out" 2>&1 ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
         fanlayout)
