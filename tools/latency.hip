@@ -38,28 +38,28 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&a, n * 4);
     (void)hipMalloc(&b, n * 4);
     (void)hipMemset(a, 0, n * 4);
-    hipMemset(b, 0, n * 4);
-    hipHostMalloc(&ha, n * 4, 0);
-    hipHostMalloc(&hb, n * 4, 0);
+    (void)hipMemset(b, 0, n * 4);
+    (void)hipHostMalloc(&ha, n * 4, 0);
+    (void)hipHostMalloc(&hb, n * 4, 0);
     std::vector<float> pa(n, 1.f), pb(n, 1.f);
     hipStream_t s;
-    hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     hipPointerAttribute_t at;
     int dev = 0;
 
     measure("empty kernel launch (host side only)", reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s); });
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     measure("empty kernel launch + hipStreamSynchronize", reps, [&] {
         hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
-        hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(s);
     });
-    measure("hipPointerGetAttributes (device ptr)", reps, [&] { hipPointerGetAttributes(&at, a); });
+    measure("hipPointerGetAttributes (device ptr)", reps, [&] { (void)hipPointerGetAttributes(&at, a); });
     measure("hipPointerGetAttributes (pageable ptr)", reps, [&] {
         if (hipPointerGetAttributes(&at, pa.data()) != hipSuccess) (void)hipGetLastError();
     });
     measure("hipGetDevice + hipSetDevice", reps, [&] {
-        hipGetDevice(&dev);
-        hipSetDevice(dev);
+        (void)hipGetDevice(&dev);
+        (void)hipSetDevice(dev);
     });
     mi::R2Args r{};
     r.acc = b;
@@ -70,18 +70,18 @@ int main(int argc, char** argv) {
     measure("reduce2_kernel direct hipLaunchKernelGGL (host side)", reps, [&] {
         hipLaunchKernelGGL((mi::reduce2_kernel<float, 0, 0u, 1, 1024>), dim3(1), dim3(1024), 0, s, r);
     });
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     measure("reduce2_kernel direct launch + hipGetLastError", reps, [&] {
         hipLaunchKernelGGL((mi::reduce2_kernel<float, 0, 0u, 1, 1024>), dim3(1), dim3(1024), 0, s, r);
         (void)hipGetLastError();
     });
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     measure("hipGetLastError alone", reps, [&] { (void)hipGetLastError(); });
     measure("mi_reduce 4 KiB (async launch, host side)", reps, [&] { mi_reduce(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, s); });
-    hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(s);
     measure("mi_reduce 4 KiB + hipStreamSynchronize", reps, [&] {
         mi_reduce(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, s);
-        hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(s);
     });
     measure("mi_reduce_sync 4 KiB device", reps, [&] { mi_reduce_sync(a, b, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
     measure("mi_reduce_sync 4 KiB pinned host (zero-copy)", reps, [&] { mi_reduce_sync(ha, hb, n, MI_FLOAT32, MI_OP_SUM, 0, -1); });
