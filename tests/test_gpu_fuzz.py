@@ -2,7 +2,7 @@
 op, semantic variant, input count 1..16, element count (empty, tiny, within
 one tile, across tiles), a different element offset per operand (common and
 differing misalignments), in place or out of place.  Each case is checked
-bit-exactly (NaN payloads aside) against the oracle's chained
+bit-exactly (bf16/fp16 NaN payloads included) against the oracle's chained
 ccl_comp_reduce fold, or its fp32-accumulate fan-in when that variant is set.
 The case list is fixed by the seed, so a failure names a reproducible case.
 """

@@ -92,6 +92,9 @@ for step in "$@"; do
             run misalign 300 python tools/misalign_probe.py ;;
         nanprobe)
             run nanprobe 300 python tools/nan_probe.py ;;
+        soak)  # a longer seeded fuzz of the device and synchronous entries (FUZZ_CASES cases)
+            MI_FUZZ_CASES=${FUZZ_CASES:-8000} run soak 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -q \
+                -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         benchall)
             for c in c3-bf16 c3-fp16 c4 c4-bf16acc c5-int32-max c5-int64-prod; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-host-leg
