@@ -168,6 +168,13 @@ __device__ __forceinline__ typename Tr<Tag>::C widen(typename Tr<Tag>::S s) {
 // round a compute value to storage: per-step / final rounding
 template <typename Tag, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::S narrow(typename Tr<Tag>::C c) {
+    // Keep the fp32 value: left alone, the compiler turns
+    // fptrunc(fmul(fpext a, fpext b)) into a native v_pk_mul_f16 (likewise
+    // adds), whose zero signs differed from VCVTPS2PH of the fp32 product on
+    // the GPU (fp16 prod chains gave +0 for -0; profiles/round2_nan/).  The
+    // kernels compute in fp32 and round with the restated conversions only;
+    // tests/test_kernel_resources.py checks the built code has no f16 math.
+    if constexpr (Tr<Tag>::lp) asm volatile("" : "+v"(c));
     if constexpr (std::is_same<Tag, bf16_tag>::value) {
         if constexpr (V & V_BF16_RNE)
             return (uint16_t)f32_to_bf16_rne<X>(c);
@@ -217,14 +224,7 @@ template <typename Tag, int OP, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::C step(typename Tr<Tag>::C x, typename Tr<Tag>::C acc) {
     auto c = apply<OP, (V & V_INOUT_FIRST) != 0>(x, acc);
     if constexpr (X && Tr<Tag>::lp && (OP == OP_SUM || OP == OP_PROD)) c = x86_nan_first(c, x, acc);
-    if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) {
-        // Keep the fp32 result: left alone, the compiler turns
-        // fptrunc(fmul(fpext a, fpext b)) into a native v_pk_mul_f16, whose
-        // zero signs differed from VCVTPS2PH of the fp32 product on the
-        // GPU (fp16 prod chains gave +0 for -0; profiles/round2_nan/).
-        asm volatile("" : "+v"(c));
-        c = widen<Tag>(narrow<Tag, V, X>(c));
-    }
+    if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) c = widen<Tag>(narrow<Tag, V, X>(c));
     return c;
 }
 
