@@ -7,6 +7,14 @@ CPU oracle on one thread (the reference's one-worker rate).  Sizes 4 KiB ..
 buffers.  One JSON line per (dtype, kind, size): best-of-reps microseconds.
 
   python tools/dispatch_sweep.py [--max-mib 512] [--dtypes f32,bf16]
+  python tools/dispatch_sweep.py --recommend [--min-kib 4 --max-mib 1024]
+
+--recommend ends with the dispatcher settings these measurements imply for
+this host (one JSON line, and `export` lines on stderr): per pointer kind,
+the largest bucket up to which the calling thread's CPU beats the GPU, and
+the CPU share of the cooperative split that moved the most bytes above it.
+The defaults in oneccl_amd/csrc/comp.cpp came from this sweep on the MI355X
+box's EPYC 9575F; another host can run it once and export the result.
 """
 from __future__ import annotations
 
@@ -35,6 +43,30 @@ def best_us(fn, reps):
     return round(min(t) * 1e6, 2), round(sorted(t)[len(t) // 2] * 1e6, 2)
 
 
+def recommend(rows):
+    """Dispatcher settings from sweep rows (dicts as printed by main()):
+    {kind: {"host_max_bytes": B, "share": S}} for each pointer kind seen."""
+    out = {}
+    for kind in sorted({r["kind"] for r in rows}):
+        rs = sorted((r for r in rows if r["kind"] == kind), key=lambda r: r["bytes"])
+        host_max = 0
+        for r in rs:  # the CPU path must beat the GPU alone and every split at every size up to it
+            alt = min([r["gpu_us"]] + [v for k, v in r.items() if k.startswith("coop") and k.endswith("_us")
+                                       and not k.endswith("median_us")])
+            if r["cpu_us"] <= alt:
+                host_max = r["bytes"]
+            else:
+                break
+        shares = sorted({float(k[4:-6]) for r in rs for k in r if k.startswith("coop") and k.endswith("_GiBps")})
+        best, best_rate = None, 0.0
+        for sh in shares:
+            rates = [r[f"coop{sh:g}_GiBps"] for r in rs if f"coop{sh:g}_GiBps" in r and r["bytes"] > host_max]
+            if rates and sum(rates) / len(rates) > best_rate:
+                best, best_rate = sh, sum(rates) / len(rates)
+        out[kind] = {"host_max_bytes": host_max, "share": best, "split_mean_GiBps": round(best_rate, 2)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-mib", type=int, default=512)
@@ -42,7 +74,9 @@ def main():
     ap.add_argument("--kinds", default="pageable,pinned")
     ap.add_argument("--shares", default="0.3,0.45,0.6")
     ap.add_argument("--min-kib", type=int, default=4)
+    ap.add_argument("--recommend", action="store_true", help="end with the dispatcher settings for this host")
     args = ap.parse_args()
+    rows = []
     import numpy as np
     import torch
 
@@ -89,9 +123,19 @@ def main():
                 row["oracle_1t_us"], _ = best_us(lambda: oracle.comp_reduce(a, b, dt, 0), reps)
                 for mode, _ in modes:
                     row[f"{mode}_GiBps"] = round(nbytes / (row[f"{mode}_us"] * 1e-6) / 2**30, 2)
+                rows.append(row)
                 print(json.dumps(row), flush=True)
     for kk in KNOBS:
         os.environ.pop(kk, None)
+    if args.recommend:
+        rec = recommend([r for r in rows if r["dtype"] == args.dtypes.split(",")[0]])
+        print(json.dumps({"recommend": rec}), flush=True)
+        env = {"pageable": ("CCL_COMP_HOST_MAX_BYTES", "CCL_COMP_HOST_SHARE"),
+               "pinned": ("CCL_COMP_HOST_MAX_PINNED_BYTES", "CCL_COMP_HOST_SHARE_PINNED")}
+        for kind, r in rec.items():
+            print(f"export {env[kind][0]}={r['host_max_bytes']}", file=sys.stderr)
+            if r["share"] is not None:
+                print(f"export {env[kind][1]}={r['share']:g}", file=sys.stderr)
 
 
 if __name__ == "__main__":
