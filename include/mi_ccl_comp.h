@@ -78,6 +78,10 @@ int mi_ccl_comp_request_free(struct ccl_comp_request* req);
 const char* mi_ccl_reduction_to_str(int op);
 /* Re-read CCL_BF16 / CCL_FP16 / CCL_COMP_HIP_DEVICE (env.cpp:711-720). */
 int mi_ccl_env_reload(void);
+/* The calling thread's CPU share of the cooperative split of host buckets
+ * above the dispatcher's threshold (pinned = 1: all operands pinned), as
+ * adapted by its own split calls; < 0 before the first one.  Diagnostic. */
+double mi_ccl_comp_split_share(int pinned);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

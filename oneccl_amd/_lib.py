@@ -7,7 +7,7 @@ library is missing: there is no CPU fallback anywhere in the product.
 from __future__ import annotations
 
 import ctypes
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint, c_void_p
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -98,6 +98,7 @@ SHIM_API = [
     ("mi_ccl_comp_request_free", c_int, [c_void_p]),
     ("mi_ccl_reduction_to_str", c_char_p, [c_int]),
     ("mi_ccl_env_reload", c_int, []),
+    ("mi_ccl_comp_split_share", c_double, [c_int]),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

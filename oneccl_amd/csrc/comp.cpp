@@ -22,6 +22,8 @@
 //                      bench (ccl_mirror.hpp; same mangled symbols).
 #include <dlfcn.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -103,7 +105,11 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
 // The defaults come from the MI355X sweeps (EPYC 9575F host, DESIGN.md §6,
 // profiles/round2_dispatch/): below 16 MiB one core beats a GPU round trip
 // (4 KiB: 1.8 vs 16.7 us); from 32 MiB up the split at 0.45 moves 32-46
-// GiB/s against 21-23 for one core and 17-25 for the GPU alone.
+// GiB/s against 21-23 for one core and 17-25 for the GPU alone.  When the
+// share is not set in the environment, each thread adapts it from the
+// rates its own split calls measure (coop_fold; CCL_COMP_HOST_SHARE_ADAPT=0
+// keeps the default fixed): the best share moved from 0.45 to 0.4 on a box
+// whose core read pinned pages at 14 instead of 22 GiB/s.
 static const size_t kHostMaxPageableDefault = 16ull << 20;
 static const size_t kHostMaxPinnedDefault = 16ull << 20;
 static const double kHostShareDefault = 0.45;
@@ -112,6 +118,7 @@ static const double kHostSharePinnedDefault = 0.45;
 struct HostMax {
     size_t pageable = 0, pinned = 0;
     double share = 0, share_pinned = 0;  // cooperative split, see coop_fold
+    bool adapt = false, adapt_pinned = false;  // shares not fixed by the environment
 };
 
 static HostMax parse_host_max() {
@@ -126,6 +133,10 @@ static HostMax parse_host_max() {
     m.share = std::min(0.95, std::max(0.0, sh ? atof(sh) : kHostShareDefault));
     m.share_pinned = std::min(0.95, std::max(0.0, shp ? atof(shp) : kHostSharePinnedDefault));
     if (m.pageable == 0) m.share = m.share_pinned = 0;  // "always the GPU"
+    const char* ad = getenv("CCL_COMP_HOST_SHARE_ADAPT");
+    const bool adapt = !(ad && atoi(ad) == 0);
+    m.adapt = adapt && !sh && m.share > 0;
+    m.adapt_pinned = adapt && !shp && m.share_pinned > 0;
     return m;
 }
 
@@ -429,7 +440,30 @@ int host_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
 // elements, so the bf16 keep-precision count % 16 tail stays in the last
 // part exactly as in the whole array.  Element-wise, so the bits are those of
 // either path alone.
-int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags, double share) {
+//
+// Adaptive share (`adapt`: not fixed by the environment).  The head runs in
+// chunks of ~8 MiB, polling the GPU part between them, so the call knows both
+// parts' durations even when the GPU finishes first; the rates give the share
+// at which both would have finished together, and the thread's share for
+// this pointer kind moves halfway there (kept within [0.1, 0.9]).  The
+// chunks are multiples of 256 elements: each is a whole head region for the
+// keep-precision tail rule, as above.
+struct SplitShare {
+    double share[2] = {-1.0, -1.0};  // [0] some operand pageable, [1] all pinned; < 0: not started
+};
+static thread_local SplitShare t_split;
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags, double share,
+              int pinned, bool adapt) {
+    double& cur = t_split.share[pinned ? 1 : 0];
+    if (adapt) {
+        if (cur < 0) cur = share;
+        share = cur;
+    }
     const size_t es = mi_dtype_size(dt);
     size_t s = (size_t)((double)count * share);
     s -= s % 256;
@@ -438,12 +472,29 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     const void* gins[MI_MAX_INPUTS];
     for (int i = 0; i < k; i++) gins[i] = static_cast<const char*>(ins[i]) + s * es;
     mi_request_t r = nullptr;
+    const double t0 = now_s();
     if (int rc = mi_reduce_start(gins, k, static_cast<char*>(out) + s * es, count - s, dt, op, flags,
                                  mi_comp_device(), &r))
         return rc;
-    const int hrc = mi_host_reduce(ins, k, out, s, dt, op, flags);
+    size_t chunk = adapt ? std::max<size_t>(256, ((size_t)8 << 20) / es) : s;
+    chunk -= chunk % 256;
+    double t_gpu = -1.0;
+    int hrc = 0;
+    for (size_t i = 0; i < s && hrc == 0; i += chunk) {
+        const void* hins[MI_MAX_INPUTS];
+        for (int j = 0; j < k; j++) hins[j] = static_cast<const char*>(ins[j]) + i * es;
+        hrc = mi_host_reduce(hins, k, static_cast<char*>(out) + i * es, std::min(chunk, s - i), dt, op, flags);
+        int done = 0;
+        if (adapt && t_gpu < 0 && mi_test(r, &done) == 0 && done) t_gpu = now_s() - t0;
+    }
+    const double t_cpu = now_s() - t0;
     const int wrc = mi_wait(r);
+    if (t_gpu < 0) t_gpu = now_s() - t0;
     (void)mi_request_free(r);
+    if (adapt && hrc == 0 && wrc == 0 && t_cpu > 0 && t_gpu > 0) {
+        const double r_cpu = (double)s / t_cpu, r_gpu = (double)(count - s) / t_gpu;
+        cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
+    }
     return wrc ? wrc : hrc;
 }
 
@@ -456,7 +507,9 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
         if (m.share > 0 || m.share_pinned > 0) {
             const int kind = host_kind(ins, k, out);
             const double share = kind == 1 ? m.share_pinned : (kind == 2 ? m.share : 0.0);
-            if (share > 0) return coop_fold(ins, k, out, count, dt, op, flags, share);
+            if (share > 0)
+                return coop_fold(ins, k, out, count, dt, op, flags, share, kind == 1,
+                                 kind == 1 ? m.adapt_pinned : m.adapt);
         }
     }
     if (devs.size() >= 2) {
@@ -972,9 +1025,12 @@ int mi_ccl_env_reload(void) {
         std::lock_guard<std::mutex> g(g_env_mu);
         parse_env_locked();
         shard_env_reload();
+        t_split = SplitShare();  // the calling thread's adapted shares start over
         return 0;
     });
 }
+
+double mi_ccl_comp_split_share(int pinned) { return t_split.share[pinned ? 1 : 0]; }
 
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl) {
     MI_SHIM_GUARD({

@@ -20,12 +20,14 @@ pytestmark = pytest.mark.gpu
 
 
 KNOBS = ("CCL_COMP_HOST_MAX_BYTES", "CCL_COMP_HOST_MAX_PINNED_BYTES", "CCL_COMP_HOST_SHARE",
-         "CCL_COMP_HOST_SHARE_PINNED")
+         "CCL_COMP_HOST_SHARE_PINNED", "CCL_COMP_HOST_SHARE_ADAPT")
 
 
 @pytest.fixture
 def threshold():
     saved = {k: os.environ.get(k) for k in KNOBS}
+    for k in KNOBS:  # every test starts from the defaults
+        os.environ.pop(k, None)
 
     def set_(v, **kv):
         os.environ["CCL_COMP_HOST_MAX_BYTES"] = str(v)
@@ -138,13 +140,20 @@ def test_cooperative_split_same_bits(kind, dt, op, threshold):
     assert_same(got, exp, dt, f"{kind} split")
 
 
+@pytest.mark.parametrize("share", ["0.5", "adapt"])
 @pytest.mark.parametrize("k", [4, 19])
-def test_cooperative_split_keep_precision_tail(k, threshold):
+def test_cooperative_split_keep_precision_tail(k, share, threshold):
     """bf16 keep-precision fan-in across the split: the count % 16 truncated
-    tail must land in the GPU's (last) part as in the whole array."""
-    threshold(1 << 20, CCL_COMP_HOST_SHARE=0.5)
+    tail must land in the GPU's (last) part as in the whole array; with an
+    adapting share the head also runs in 8 MiB chunks, none of which may
+    truncate."""
+    if share == "adapt":
+        threshold(1 << 20)
+        n = (12 << 20) + 11
+    else:
+        threshold(1 << 20, CCL_COMP_HOST_SHARE=share)
+        n = (3 << 20) + 11
     b_impl, _ = comp.impl_types()
-    n = (3 << 20) + 11
     ins = [rand_array(BF16, n, seed=500 + j, specials=False) for j in range(k)]
     packed = np.concatenate(ins)
     offsets = [j * n for j in range(k)]
@@ -154,3 +163,57 @@ def test_cooperative_split_keep_precision_tail(k, threshold):
     comp.comp_batch_reduce(packed.ctypes.data, offsets, n, got.ctypes.data, comp.datatype.bfloat16,
                            comp.reduction.sum, 1)
     assert_same(got, exp, BF16)
+
+
+def _split_share(pinned):
+    from oneccl_amd import _lib
+    return _lib.shim().mi_ccl_comp_split_share(1 if pinned else 0)
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+@pytest.mark.parametrize("dt", [FP32, BF16])
+def test_adaptive_split_keeps_bits_and_bounds_its_share(kind, dt, threshold):
+    """With the CPU share left to the dispatcher (no CCL_COMP_HOST_SHARE*),
+    each split call times both parts and moves the thread's share toward the
+    balance point: every call still gives the oracle's bits, and the share
+    stays within [0.1, 0.9]."""
+    import torch
+    threshold(1 << 20)
+    b_impl, f_impl = comp.impl_types()
+    es = np.dtype(oracle.NP_DTYPE[dt]).itemsize
+    n = (48 << 20) // es + 13
+    a = rand_array(dt, n, seed=91, specials=False)
+    b0 = rand_array(dt, n, seed=92, specials=False)
+    exp = b0.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, int(b_impl), int(f_impl))
+    assert _split_share(kind == "pinned") < 0  # env_reload started this thread over
+    if kind == "pinned":
+        ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        tb = torch.empty(n * es, dtype=torch.uint8).pin_memory()
+        pa, pb = ta.data_ptr(), tb.data_ptr()
+        hb = tb.numpy().view(exp.dtype)
+    else:
+        ta, hb = a, np.empty_like(b0)
+        pa, pb = a.ctypes.data, hb.ctypes.data
+    shares = []
+    for i in range(6):
+        hb[:] = b0
+        comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+        assert_same(hb, exp, dt, f"{kind} call {i}")
+        shares.append(_split_share(kind == "pinned"))
+    assert all(0.1 <= s <= 0.9 for s in shares), shares
+    assert _split_share(kind != "pinned") < 0  # the other pointer kind's share is its own
+
+
+@pytest.mark.parametrize("env", [{"CCL_COMP_HOST_SHARE": "0.45", "CCL_COMP_HOST_SHARE_PINNED": "0.45"},
+                                 {"CCL_COMP_HOST_SHARE_ADAPT": "0"}], ids=["fixed-share", "adapt-off"])
+def test_fixed_share_does_not_adapt(env, threshold):
+    threshold(1 << 20, **env)
+    n = (24 << 20) // 4
+    a = rand_array(FP32, n, seed=93, specials=False)
+    b = rand_array(FP32, n, seed=94, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+    assert_same(b, exp, FP32)
+    assert _split_share(False) < 0

@@ -114,8 +114,11 @@ def test_intree_object_needs_nothing_the_tree_does_not_provide(objs):
     provided = set().union(*(_undefs(objs[n][0]) for n in REPLACED))  # already resolved inside libccl
     provided |= _global_defs(objs["datatype"][0])  # ccl_datatype's constructor
     provided |= _dyn_defs(str(ROOT / "oneccl_amd" / "lib" / "libmi_reduce.so"))
+    # ld.so: __tls_get_addr, which libccl's own thread_locals need as well
+    # (src/common/log/log.cpp, src/common/global/global.cpp)
     for lib in ("/lib/x86_64-linux-gnu/libc.so.6", "/lib/x86_64-linux-gnu/libstdc++.so.6",
-                "/lib/x86_64-linux-gnu/libgcc_s.so.1", "/lib/x86_64-linux-gnu/libm.so.6"):
+                "/lib/x86_64-linux-gnu/libgcc_s.so.1", "/lib/x86_64-linux-gnu/libm.so.6",
+                "/lib64/ld-linux-x86-64.so.2"):
         if Path(lib).exists():
             provided |= _dyn_defs(lib)
     libgcc = subprocess.run(["g++", "-print-libgcc-file-name"], capture_output=True, text=True).stdout.strip()

@@ -8,6 +8,12 @@ buffers.  One JSON line per (dtype, kind, size): best-of-reps microseconds.
 
   python tools/dispatch_sweep.py [--max-mib 512] [--dtypes f32,bf16]
   python tools/dispatch_sweep.py --recommend [--min-kib 4 --max-mib 1024]
+  python tools/dispatch_sweep.py --adapt-trace [--max-mib 256]
+
+--adapt-trace follows the adaptive split (no CCL_COMP_HOST_SHARE* set): for
+one bucket of --max-mib per pointer kind, 12 consecutive ccl_comp_reduce
+calls on one thread, each line the share it ran with, the share it left and
+its GiB/s.
 
 --recommend ends with the dispatcher settings these measurements imply for
 this host (one JSON line, and `export` lines on stderr): per pointer kind,
@@ -67,6 +73,43 @@ def recommend(rows):
     return out
 
 
+def adapt_trace(args):
+    import numpy as np
+    import torch
+
+    from oneccl_amd import _lib, comp
+    shim = _lib.shim()
+    for kk in KNOBS:
+        os.environ.pop(kk, None)
+    nbytes = args.max_mib << 20
+    for dname in args.dtypes.split(","):
+        dt, es = DT[dname]
+        n = nbytes // es
+        for kind in args.kinds.split(","):
+            comp.env_reload()
+            if kind == "pinned":
+                ta = torch.full((nbytes,), 0x3F, dtype=torch.uint8).pin_memory()
+                tb = torch.full((nbytes,), 0x3F, dtype=torch.uint8).pin_memory()
+                pa, pb = ta.data_ptr(), tb.data_ptr()
+            else:
+                a = np.full(nbytes, 0x3F, np.uint8)
+                b = np.full(nbytes, 0x3F, np.uint8)
+                pa, pb = a.ctypes.data, b.ctypes.data
+            for i in range(12):
+                before = shim.mi_ccl_comp_split_share(1 if kind == "pinned" else 0)
+                t0 = time.perf_counter()
+                comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+                dt_s = time.perf_counter() - t0
+                print(json.dumps({"dtype": dname, "kind": kind, "bytes": nbytes, "call": i,
+                                  "share_in": round(before, 4),
+                                  "share_out": round(shim.mi_ccl_comp_split_share(1 if kind == "pinned" else 0), 4),
+                                  "GiBps": round(nbytes / dt_s / 2**30, 2)}), flush=True)
+                if kind != "pinned":
+                    b[:] = 0x3F  # keep the values away from overflow and denormals
+                else:
+                    tb.fill_(0x3F)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-mib", type=int, default=512)
@@ -75,7 +118,10 @@ def main():
     ap.add_argument("--shares", default="0.3,0.45,0.6")
     ap.add_argument("--min-kib", type=int, default=4)
     ap.add_argument("--recommend", action="store_true", help="end with the dispatcher settings for this host")
+    ap.add_argument("--adapt-trace", action="store_true", help="follow the adaptive split over 12 calls")
     args = ap.parse_args()
+    if args.adapt_trace:
+        return adapt_trace(args)
     rows = []
     import numpy as np
     import torch
