@@ -445,11 +445,15 @@ int host_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
 // chunks of ~8 MiB, polling the GPU part between them, so the call knows both
 // parts' durations even when the GPU finishes first; the rates give the share
 // at which both would have finished together, and the thread's share for
-// this pointer kind moves halfway there (kept within [0.1, 0.9]).  The
+// this pointer kind moves halfway there (kept within [0.1, 0.9]).  A thread's
+// first split call of a kind only warms up: it pays for the staging buffers
+// and the worker thread, which made it read as a GPU 10x slower than it is
+// (profiles/round2_dispatch/adapt_trace.jsonl).  The
 // chunks are multiples of 256 elements: each is a whole head region for the
 // keep-precision tail rule, as above.
 struct SplitShare {
     double share[2] = {-1.0, -1.0};  // [0] some operand pageable, [1] all pinned; < 0: not started
+    unsigned calls[2] = {0, 0};
 };
 static thread_local SplitShare t_split;
 
@@ -460,6 +464,7 @@ static double now_s() {
 int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags, double share,
               int pinned, bool adapt) {
     double& cur = t_split.share[pinned ? 1 : 0];
+    unsigned& calls = t_split.calls[pinned ? 1 : 0];
     if (adapt) {
         if (cur < 0) cur = share;
         share = cur;
@@ -491,7 +496,7 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     const int wrc = mi_wait(r);
     if (t_gpu < 0) t_gpu = now_s() - t0;
     (void)mi_request_free(r);
-    if (adapt && hrc == 0 && wrc == 0 && t_cpu > 0 && t_gpu > 0) {
+    if (adapt && calls++ > 0 && hrc == 0 && wrc == 0 && t_cpu > 0 && t_gpu > 0) {
         const double r_cpu = (double)s / t_cpu, r_gpu = (double)(count - s) / t_gpu;
         cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
     }
