@@ -108,6 +108,26 @@ def adapt_trace(args):
                     b[:] = 0x3F  # keep the values away from overflow and denormals
                 else:
                     tb.fill_(0x3F)
+            # the same buffers at fixed shares: where the adapted share should have landed
+            env = "CCL_COMP_HOST_SHARE_PINNED" if kind == "pinned" else "CCL_COMP_HOST_SHARE"
+            fixed = {}
+            for sh in args.shares.split(","):
+                os.environ[env] = sh
+                comp.env_reload()
+                best = float("inf")
+                for i in range(4):
+                    t0 = time.perf_counter()
+                    comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+                    if i:
+                        best = min(best, time.perf_counter() - t0)
+                    if kind != "pinned":
+                        b[:] = 0x3F
+                    else:
+                        tb.fill_(0x3F)
+                fixed[sh] = round(nbytes / best / 2**30, 2)
+            os.environ.pop(env, None)
+            comp.env_reload()
+            print(json.dumps({"dtype": dname, "kind": kind, "bytes": nbytes, "fixed_share_GiBps": fixed}), flush=True)
 
 
 def main():

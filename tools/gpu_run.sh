@@ -78,7 +78,8 @@ for step in "$@"; do
         dispatch)
             run dispatch 600 python tools/dispatch_sweep.py --max-mib ${DISPATCH_MAX_MIB:-512} ;;
         adapt)  # the adaptive split followed over 12 calls per pointer kind
-            run adapt 300 python tools/dispatch_sweep.py --adapt-trace --max-mib 256 --dtypes f32,bf16 ;;
+            run adapt 400 python tools/dispatch_sweep.py --adapt-trace --max-mib 256 --dtypes f32,bf16 \
+                --shares 0.3,0.35,0.4,0.45,0.5,0.55 ;;
         coop)  # the cooperative split above the crossover, shares swept
             run coop 600 python tools/dispatch_sweep.py --min-kib 16384 --max-mib 1024 --shares 0.2,0.3,0.4,0.5,0.6 ;;
         dist2)
