@@ -82,6 +82,11 @@ int mi_ccl_env_reload(void);
  * above the dispatcher's threshold (pinned = 1: all operands pinned), as
  * adapted by its own split calls; < 0 before the first one.  Diagnostic. */
 double mi_ccl_comp_split_share(int pinned);
+/* Threads the dispatcher counts as reducing host buckets now: inside such a
+ * call, or returned from one within the last 50 ms.  A host bucket above the
+ * threshold is split with the GPU only while this is at most
+ * CCL_COMP_HOST_SPLIT_WORKERS (pageable) / _PINNED.  Diagnostic. */
+int mi_ccl_comp_host_workers(void);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

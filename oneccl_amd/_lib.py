@@ -99,6 +99,7 @@ SHIM_API = [
     ("mi_ccl_reduction_to_str", c_char_p, [c_int]),
     ("mi_ccl_env_reload", c_int, []),
     ("mi_ccl_comp_split_share", c_double, [c_int]),
+    ("mi_ccl_comp_host_workers", c_int, []),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

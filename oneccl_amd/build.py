@@ -126,6 +126,15 @@ def build_latency(force: bool = False) -> Path:
     return out
 
 
+def build_segv_trace(force: bool = False) -> Path:
+    """Diagnostic: tools/libsegv_trace.so prints a native backtrace on SIGSEGV."""
+    out = ROOT / "tools" / "libsegv_trace.so"
+    src = ROOT / "tools" / "segv_trace.c"
+    if src.exists() and (force or _stale(out, [src])):
+        _run(["gcc", "-O1", "-g", "-fPIC", "-shared", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
 def build_dropin_caller(force: bool = False) -> Path:
     """Test program: a C++ caller linking libccl_comp_hip.so by oneCCL's own
     mangled names (tests/cpp/dropin_caller.cpp)."""
@@ -199,6 +208,7 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_fan_sweep()
     build_burst_sweep()
     build_latency()
+    build_segv_trace()
     if asan:
         build_asan(force)
 

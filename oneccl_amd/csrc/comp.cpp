@@ -23,6 +23,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -110,15 +111,27 @@ std::map<ccl_fp16_impl_type, std::string> fp16_env_impl_names = {
 // rates its own split calls measure (coop_fold; CCL_COMP_HOST_SHARE_ADAPT=0
 // keeps the default fixed): the best share moved from 0.45 to 0.4 on a box
 // whose core read pinned pages at 14 instead of 22 GiB/s.
+// Several threads may reduce host buckets at once (oneCCL's CCL_WORKER_COUNT
+// workers, worker.cpp:310-379), and they share one PCIe link and the host's
+// DRAM.  CCL_COMP_HOST_SPLIT_WORKERS (pageable) / _PINNED caps the number of
+// such threads (host_workers) up to which a bucket is still split; beyond it
+// every bucket stays on its thread's CPU.  Default 0 = no cap: in paired
+// rounds on MI355X boxes the split never lost to all-CPU at 1-16 workers,
+// 64 MiB buckets (+10-80 %; profiles/round2_dispatch/workers_paired_*,
+// DESIGN.md §6).  The cap is for hosts whose DRAM the staging copies would
+// saturate first.
 static const size_t kHostMaxPageableDefault = 16ull << 20;
 static const size_t kHostMaxPinnedDefault = 16ull << 20;
 static const double kHostShareDefault = 0.45;
 static const double kHostSharePinnedDefault = 0.45;
+static const int kSplitWorkersDefault = 0;
+static const int kSplitWorkersPinnedDefault = 0;
 
 struct HostMax {
     size_t pageable = 0, pinned = 0;
     double share = 0, share_pinned = 0;  // cooperative split, see coop_fold
     bool adapt = false, adapt_pinned = false;  // shares not fixed by the environment
+    int split_workers = 0, split_workers_pinned = 0;  // 0 = split whatever the number of workers
 };
 
 static HostMax parse_host_max() {
@@ -137,6 +150,10 @@ static HostMax parse_host_max() {
     const bool adapt = !(ad && atoi(ad) == 0);
     m.adapt = adapt && !sh && m.share > 0;
     m.adapt_pinned = adapt && !shp && m.share_pinned > 0;
+    const char* sw = getenv("CCL_COMP_HOST_SPLIT_WORKERS");
+    const char* swp = getenv("CCL_COMP_HOST_SPLIT_WORKERS_PINNED");
+    m.split_workers = std::max(0, sw ? atoi(sw) : kSplitWorkersDefault);
+    m.split_workers_pinned = std::max(0, swp ? atoi(swp) : kSplitWorkersPinnedDefault);
     return m;
 }
 
@@ -503,18 +520,70 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     return wrc ? wrc : hrc;
 }
 
+// Threads reducing host buckets: each caller of a host-bucket fold owns a
+// slot, marked while the call runs and stamped when it returns.  A thread
+// counts as a worker while it is inside such a call or returned from one
+// within the last kSeenWindowNs, so oneCCL's workers, which reduce chunk
+// after chunk, are counted across the gaps between their calls.
+constexpr int kSeenSlots = 64;
+constexpr int64_t kSeenWindowNs = 50 * 1000 * 1000;
+struct alignas(64) SeenSlot {  // one cache line per slot
+    std::atomic<int64_t> last_ns;
+    std::atomic<int> inside;
+};
+static SeenSlot g_seen[kSeenSlots];
+static std::atomic<unsigned> g_seen_next(0);
+static thread_local int t_seen = -1;
+
+static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct HostCall {
+    int slot;
+    HostCall() {
+        if (t_seen < 0) t_seen = (int)(g_seen_next.fetch_add(1, std::memory_order_relaxed) % kSeenSlots);
+        slot = t_seen;
+        g_seen[slot].inside.fetch_add(1, std::memory_order_relaxed);
+    }
+    ~HostCall() {
+        g_seen[slot].last_ns.store(now_ns(), std::memory_order_relaxed);
+        g_seen[slot].inside.fetch_sub(1, std::memory_order_relaxed);
+    }
+};
+
+int host_workers() {
+    const int64_t t = now_ns();
+    int n = 0;
+    for (int i = 0; i < kSeenSlots; i++) {
+        const SeenSlot& s = g_seen[i];
+        if (s.inside.load(std::memory_order_relaxed) > 0) n++;
+        else {
+            const int64_t last = s.last_ns.load(std::memory_order_relaxed);
+            if (last != 0 && t - last < kSeenWindowNs) n++;
+        }
+    }
+    return n;
+}
+
 int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags) {
     const size_t bytes = count * mi_dtype_size(dt);
-    if (host_path(ins, k, out, bytes)) return host_fold(ins, k, out, count, dt, op, flags);
+    const HostMax m = mi_host_max();
+    // 0: some operand is device memory (or the dispatcher is off), 1: all
+    // pinned, 2: host memory, some of it pageable
+    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
     const std::vector<int> devs = shard_devices();
-    if (devs.size() < 2) {
-        const HostMax m = mi_host_max();
-        if (m.share > 0 || m.share_pinned > 0) {
-            const int kind = host_kind(ins, k, out);
-            const double share = kind == 1 ? m.share_pinned : (kind == 2 ? m.share : 0.0);
-            if (share > 0)
-                return coop_fold(ins, k, out, count, dt, op, flags, share, kind == 1,
-                                 kind == 1 ? m.adapt_pinned : m.adapt);
+    if (kind != 0) {
+        HostCall call;  // this thread counts among the host-bucket workers
+        const size_t lim = kind == 1 ? m.pinned : m.pageable;
+        if (lim > 0 && bytes <= lim) return host_fold(ins, k, out, count, dt, op, flags);
+        const double share = kind == 1 ? m.share_pinned : m.share;
+        if (devs.size() < 2 && share > 0) {
+            const int limit = kind == 1 ? m.split_workers_pinned : m.split_workers;
+            if (limit > 0 && host_workers() > limit) return host_fold(ins, k, out, count, dt, op, flags);
+            return coop_fold(ins, k, out, count, dt, op, flags, share, kind == 1,
+                             kind == 1 ? m.adapt_pinned : m.adapt);
         }
     }
     if (devs.size() >= 2) {
@@ -1036,6 +1105,8 @@ int mi_ccl_env_reload(void) {
 }
 
 double mi_ccl_comp_split_share(int pinned) { return t_split.share[pinned ? 1 : 0]; }
+
+int mi_ccl_comp_host_workers(void) { return host_workers(); }
 
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl) {
     MI_SHIM_GUARD({

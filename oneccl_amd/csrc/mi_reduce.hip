@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
@@ -610,13 +611,36 @@ struct Drain {
     ~Drain() { (void)finish(); }
 };
 
+// Process exit against threads that are still exiting.  A thread's contexts
+// are freed by its thread_local destructors (hipFree of the staging buffers
+// synchronises the device and takes milliseconds).  A host program may exit
+// while such a thread is still in them: Python's Thread.join(), for one,
+// returns before the OS thread has run its thread_local destructors.  The
+// HIP runtime's own exit-time teardown then pulls the device from under
+// those calls (a SIGSEGV inside libamdhip64 from __call_tls_dtors).  So an
+// exit handler, registered after the runtime's (at the first context, when
+// HIP is initialised, so it runs before them), marks the process as exiting
+// and waits up to 2 s for teardowns already in HIP calls; later ones leave
+// their contexts to the process's end.
+std::atomic<bool> g_exiting{false};
+std::atomic<int> g_teardowns{0};
+
+void at_process_exit() {
+    g_exiting.store(true);
+    for (int i = 0; i < 2000 && g_teardowns.load() > 0; i++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+}
+
 struct ThreadCtx {
     std::vector<DevCtx*> devs;
     ~ThreadCtx() {
-        for (DevCtx* d : devs) delete d;
+        g_teardowns.fetch_add(1);
+        if (!g_exiting.load())
+            for (DevCtx* d : devs) delete d;
+        g_teardowns.fetch_sub(1);
     }
 };
 thread_local ThreadCtx t_ctx;
+std::once_flag g_exit_hook;
 
 int get_ctx(int device, DevCtx** out) {
     if (device < 0) MI_HIP(hipGetDevice(&device));
@@ -633,6 +657,7 @@ int get_ctx(int device, DevCtx** out) {
             ~Restore() { (void)hipSetDevice(dev); }
         } restore{prev};
         MI_HIP(hipSetDevice(device));
+        std::call_once(g_exit_hook, [] { std::atexit(at_process_exit); });
         std::unique_ptr<DevCtx> d(new DevCtx());
         d->device = device;
         for (int s = 0; s < 2; s++) MI_HIP(hipStreamCreateWithFlags(&d->stream[s], hipStreamNonBlocking));

@@ -20,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 
 KNOBS = ("CCL_COMP_HOST_MAX_BYTES", "CCL_COMP_HOST_MAX_PINNED_BYTES", "CCL_COMP_HOST_SHARE",
-         "CCL_COMP_HOST_SHARE_PINNED", "CCL_COMP_HOST_SHARE_ADAPT")
+         "CCL_COMP_HOST_SHARE_PINNED", "CCL_COMP_HOST_SHARE_ADAPT", "CCL_COMP_HOST_SPLIT_WORKERS",
+         "CCL_COMP_HOST_SPLIT_WORKERS_PINNED")
 
 
 @pytest.fixture
@@ -177,8 +178,11 @@ def test_adaptive_split_keeps_bits_and_bounds_its_share(kind, dt, threshold):
     each split call times both parts and moves the thread's share toward the
     balance point: every call still gives the oracle's bits, and the share
     stays within [0.1, 0.9]."""
+    import time
+
     import torch
     threshold(1 << 20)
+    time.sleep(0.06)  # other tests' worker threads leave the dispatcher's 50 ms window
     b_impl, f_impl = comp.impl_types()
     es = np.dtype(oracle.NP_DTYPE[dt]).itemsize
     n = (48 << 20) // es + 13
@@ -217,3 +221,51 @@ def test_fixed_share_does_not_adapt(env, threshold):
     comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype.float32, comp.reduction.sum)
     assert_same(b, exp, FP32)
     assert _split_share(False) < 0
+
+
+@pytest.mark.parametrize("limit", ["2", "0"], ids=["limit-2", "no-limit"])
+def test_split_yields_to_concurrent_workers(limit, threshold):
+    """oneCCL reduces from CCL_WORKER_COUNT threads at once.  Once more than
+    CCL_COMP_HOST_SPLIT_WORKERS threads reduce host buckets, a large pageable
+    bucket stays on its thread's CPU (the GPU's share of the shared host DRAM
+    and PCIe link no longer adds); with the limit off (0) every thread
+    splits.  Bits are the oracle's either way."""
+    import threading
+    import time
+    from oneccl_amd import _lib
+    threshold(1 << 20, CCL_COMP_HOST_SPLIT_WORKERS=limit)
+    time.sleep(0.06)
+    w, n = 4, (6 << 20) // 4 + 5
+    go = threading.Barrier(w)
+    shares, errs = [None] * w, []
+
+    def worker(i):
+        try:
+            a = rand_array(FP32, n, seed=300 + i, specials=False)
+            b0 = rand_array(FP32, n, seed=400 + i, specials=False)
+            exp = b0.copy()
+            oracle.comp_reduce_mt(a, exp, FP32, 0, 4)
+            small = np.ones(1024, np.float32)
+            go.wait()
+            # every thread is seen as a worker first (a CPU-path reduce)
+            comp.comp_reduce(small.ctypes.data, 1024, small.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+            go.wait()
+            for r in range(3):
+                b = b0.copy()
+                comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+                assert_same(b, exp, FP32, f"worker {i} round {r}")
+            shares[i] = _lib.shim().mi_ccl_comp_split_share(0)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+            go.abort()
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(w)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    if limit == "2":  # 4 workers > 2: nobody split
+        assert all(s < 0 for s in shares), shares
+    else:
+        assert all(0.1 <= s <= 0.9 for s in shares), shares

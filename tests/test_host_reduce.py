@@ -284,3 +284,41 @@ def test_narrower_isa_forms(isa):
                        timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout
+
+
+def test_dropin_counts_host_bucket_workers(env):
+    """The dispatcher counts the threads reducing host buckets (inside a call,
+    or returned from one within the last 50 ms): the number of oneCCL workers
+    it uses to decide whether a large pageable bucket may still be split with
+    the GPU (CCL_COMP_HOST_SPLIT_WORKERS)."""
+    import threading
+    import time
+    env()
+    s = _lib.shim()
+    time.sleep(0.06)  # earlier tests' callers leave the window
+    assert s.mi_ccl_comp_host_workers() == 0
+    w = 5
+    go = threading.Barrier(w)
+    errs = []
+
+    def worker(seed):
+        try:
+            a = rand_array(FP32, 4096, seed=seed)
+            b = rand_array(FP32, 4096, seed=seed + 1)
+            exp = b.copy()
+            oracle.comp_reduce(a, exp, FP32, 0)
+            go.wait()
+            comp.comp_reduce(a.ctypes.data, a.size, b.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+            assert_same(b, exp, FP32)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(10 * i,)) for i in range(w)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert s.mi_ccl_comp_host_workers() == w
+    time.sleep(0.06)
+    assert s.mi_ccl_comp_host_workers() == 0

@@ -81,7 +81,13 @@ for step in "$@"; do
             run adapt 400 python tools/dispatch_sweep.py --adapt-trace --max-mib 256 --dtypes f32,bf16 \
                 --shares 0.3,0.35,0.4,0.45,0.5,0.55 ;;
         workers)  # W concurrent worker threads through ccl_comp_reduce on host buckets, vs W oracle threads
-            run workers 600 python tools/workers_sweep.py --workers ${WORKERS:-1,2,4,8,16} --mib ${WORKERS_MIB:-8,64} ;;
+            run workers 600 python tools/workers_sweep.py --segv-trace --workers ${WORKERS:-1,2,4,8,16} \
+                --mib ${WORKERS_MIB:-8,64} --modes ${WORKERS_MODES:-oracle,host,split,default} &&
+            run workers_pinned 600 python tools/workers_sweep.py --segv-trace --pinned --workers ${WORKERS:-1,2,4,8,16} \
+                --mib ${WORKERS_MIB:-64} --modes ${WORKERS_MODES:-oracle,host,split,default} ;;
+        dispatchtests)
+            run pytest_dispatch 600 python -u -m pytest tests/test_gpu_dispatch.py tests/test_host_reduce.py -m "gpu or not gpu" \
+                -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         coop)  # the cooperative split above the crossover, shares swept
             run coop 600 python tools/dispatch_sweep.py --min-kib 16384 --max-mib 1024 --shares 0.2,0.3,0.4,0.5,0.6 ;;
         dist2)
