@@ -540,14 +540,16 @@ static int64_t now_ns() {
         .count();
 }
 
-struct HostCall {
-    int slot;
-    HostCall() {
+struct HostCall {  // marks the calling thread as reducing a host bucket while `on`
+    int slot = -1;
+    explicit HostCall(bool on) {
+        if (!on) return;
         if (t_seen < 0) t_seen = (int)(g_seen_next.fetch_add(1, std::memory_order_relaxed) % kSeenSlots);
         slot = t_seen;
         g_seen[slot].inside.fetch_add(1, std::memory_order_relaxed);
     }
     ~HostCall() {
+        if (slot < 0) return;
         g_seen[slot].last_ns.store(now_ns(), std::memory_order_relaxed);
         g_seen[slot].inside.fetch_sub(1, std::memory_order_relaxed);
     }
@@ -574,8 +576,8 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     // pinned, 2: host memory, some of it pageable
     const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
     const std::vector<int> devs = shard_devices();
+    const HostCall call(kind != 0);  // the thread counts among the host-bucket workers
     if (kind != 0) {
-        HostCall call;  // this thread counts among the host-bucket workers
         const size_t lim = kind == 1 ? m.pinned : m.pageable;
         if (lim > 0 && bytes <= lim) return host_fold(ins, k, out, count, dt, op, flags);
         const double share = kind == 1 ? m.share_pinned : m.share;
