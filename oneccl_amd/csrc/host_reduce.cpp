@@ -42,6 +42,7 @@
 namespace {
 
 constexpr int kChunk = 512;  // elements per fold block: the accumulator stays in L1
+constexpr int kFanChunk = 2048;  // K-input fold of 1-8-byte types: 2-16 KiB of output per block
 
 struct bf16_t {};
 struct fp16_t {};
@@ -211,6 +212,21 @@ void fold(const void* const* inputs, int k, void* out, size_t count, unsigned v)
         const C* x = static_cast<const C*>(inputs[1]);
         C* o = static_cast<C*>(out);
         for (size_t i = 0; i < count; i++) o[i] = op1<OP, INOUT_FIRST, false>(x[i], a[i]);
+        return;
+    }
+    if (!lp) {  // fan-in: every input read once, per L1-sized block of an accumulator
+        bool alias = false;  // out is also a later input: fold into a copy, store after every read
+        for (int j = 1; j < k; j++) alias = alias || inputs[j] == out;
+        alignas(64) C acc[kFanChunk];
+        for (size_t b = 0; b < count; b += kFanChunk) {
+            const size_t n = std::min<size_t>(kFanChunk, count - b);
+            C* o = alias ? acc : static_cast<C*>(out) + b;
+            const C* a = static_cast<const C*>(inputs[0]) + b;
+            const C* x = static_cast<const C*>(inputs[1]) + b;
+            for (size_t i = 0; i < n; i++) o[i] = op1<OP, INOUT_FIRST, false>(x[i], a[i]);
+            for (int j = 2; j < k; j++) apply<OP, INOUT_FIRST, false>(static_cast<const C*>(inputs[j]) + b, o, n);
+            if (alias) memcpy(static_cast<C*>(out) + b, acc, n * sizeof(C));
+        }
         return;
     }
     alignas(64) C acc[kChunk];

@@ -322,3 +322,22 @@ def test_dropin_counts_host_bucket_workers(env):
     assert s.mi_ccl_comp_host_workers() == w
     time.sleep(0.06)
     assert s.mi_ccl_comp_host_workers() == 0
+
+
+@pytest.mark.parametrize("dt", [FP32, 4, 6, FP64], ids=["f32", "i32", "i64", "f64"])
+@pytest.mark.parametrize("alias", [None, 0, 2])
+def test_host_fanin_out_aliasing(dt, alias):
+    """The K-input host fold is a function of the inputs' values before the
+    call, wherever `out` points: a distinct buffer, input 0 (in place, the
+    batch reduce's accumulator) or a later input (same bits as the GPU fan
+    kernel, which loads every input before its store)."""
+    k, n = 5, 5000 + 3
+    ins = [rand_array(dt, n, seed=60 + j, specials=False) for j in range(k)]
+    exp = ins[0].copy()
+    for j in range(1, k):
+        oracle.comp_reduce(ins[j], exp, dt, 0)
+    bufs = [x.copy() for x in ins]
+    out = np.zeros_like(ins[0]) if alias is None else bufs[alias]
+    arr = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+    assert _lib.shim().mi_host_reduce(arr, k, out.ctypes.data, n, dt, 0, 0) == 0
+    assert_same(out, exp, dt, f"alias={alias}")
