@@ -786,3 +786,39 @@ def test_keep_precision_custom_reduction():
     assert _lib.shim().mi_ccl_comp_batch_reduce_custom(ptr(packed), offs, k, n, ptr(ins[0].copy()), None, BF16, 1,
                                                        null_fn) == -1
     assert b"callback" in _lib.shim().mi_ccl_last_error()
+
+
+_EXIT_RACE = r'''
+import sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from oneccl_amd import comp
+n = (40 << 20) // 4
+def work(i):
+    a = np.full(n, 1.0, np.float32)
+    b = np.full(n, float(i), np.float32)
+    comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+    assert b[0] == i + 1.0 and b[-1] == i + 1.0
+ts = [threading.Thread(target=work, args=(i,)) for i in range(12)]
+for t in ts: t.start()
+for t in ts: t.join()
+print("exit-race: ok", flush=True)
+'''
+
+
+def test_process_exit_while_worker_threads_tear_down():
+    """Worker threads that staged pageable buckets through the GPU free their
+    contexts (hipFree of staging buffers) in thread_local destructors, which
+    Python's Thread.join() does not wait for; the process then exits at once.
+    Before the library's exit handler this died with SIGSEGV inside
+    libamdhip64 (profiles/round2_dispatch/exit_crash_trace.txt)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parent.parent)
+    env = dict(os.environ, CCL_COMP_HOST_MAX_BYTES="0")  # every bucket through the GPU's staging path
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", _EXIT_RACE, root], capture_output=True, text=True, timeout=120,
+                           env=env)
+        assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        assert "exit-race: ok" in r.stdout
