@@ -16,7 +16,7 @@
 //   fan_kernel the library's kernel (baseline)
 //   fan_kernel over one 8 GiB allocation (inputs contiguous in memory)
 //
-//   fan_sweep [bucket_MiB=1024] [rounds=5] [reps=8]
+//   fan_sweep [bucket_MiB=1024] [rounds=5] [reps=8] [layout|pipe|skew]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -139,6 +139,46 @@ __global__ __launch_bounds__(B) void pipe_kernel(RKArgs a) {
         if (tn >= ntiles) break;
         t = tn;
     }
+}
+
+// Skewed read-only K streams (skew mode): block b reads vector v of input j
+// at (v + j * skew) mod nvec, so at any moment the K streams are at K
+// different offsets instead of one.  Every byte of every input is still read
+// exactly once.  Tests whether the multi-stream read penalty (8 streams 6.4-6.8
+// TB/s vs 2 streams 7.0) comes from the K streams meeting in the same DRAM
+// banks at the same offset.
+template <int K>
+__global__ __launch_bounds__(1024) void readk_skew_kernel(RKArgs a, uint64_t skew, float* sink) {
+    const uint64_t v = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    if (v >= a.nvec) return;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        uint64_t w = v + (uint64_t)j * skew;
+        if (w >= a.nvec) w -= a.nvec;
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in[j]) + w);
+        acc ^= x[0] ^ x[1] ^ x[2] ^ x[3];
+    }
+    if (acc == 0x9e3779b9u) sink[blockIdx.x] = 1.f;
+}
+
+// The fan-in with the same skew: input j's tile t is folded with the other
+// inputs' tile t only in the unskewed kernel; here each block folds
+// (v + j*skew) of input j into out[v], which is NOT the reduce's result — a
+// timing probe of the access pattern with the store included, never a product
+// kernel.
+template <int K>
+__global__ __launch_bounds__(1024) void fan_skew_probe(RKArgs a, uint64_t skew) {
+    const uint64_t v = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    if (v >= a.nvec) return;
+    f32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        uint64_t w = v + (uint64_t)j * skew;
+        if (w >= a.nvec) w -= a.nvec;
+        acc = acc + __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in[j]) + w));
+    }
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, acc), reinterpret_cast<u32x4*>(a.out) + v);
 }
 
 struct Variant {
@@ -295,12 +335,28 @@ void add_pipe(std::vector<Variant>& vs, const RKArgs& r, unsigned grid, double b
                   }, {}});
 }
 
+template <int K>
+void add_skew(std::vector<Variant>& vs, const RKArgs& r, float* sink, double bytes, uint64_t skew, bool store) {
+    const uint64_t blocks = (r.nvec + 1023) / 1024;
+    char name[160];
+    snprintf(name, sizeof name, "%s K=%d skew=%llu vectors (%llu KiB)", store ? "fan_skew_probe" : "readk_skew", K,
+             (unsigned long long)skew, (unsigned long long)(skew * 16 / 1024));
+    vs.push_back({name, (K + (store ? 1 : 0)) * bytes, [r, blocks, sink, skew, store](hipStream_t s) {
+                      if (store)
+                          hipLaunchKernelGGL(fan_skew_probe<K>, dim3((unsigned)blocks), dim3(1024), 0, s, r, skew);
+                      else
+                          hipLaunchKernelGGL(readk_skew_kernel<K>, dim3((unsigned)blocks), dim3(1024), 0, s, r, skew,
+                                             sink);
+                  }, {}});
+}
+
 int main(int argc, char** argv) {
     const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
     const int reps = argc > 3 ? atoi(argv[3]) : 8;
     const bool layout_mode = argc > 4 && std::string(argv[4]) == "layout";
     const bool pipe_mode = argc > 4 && std::string(argv[4]) == "pipe";
+    const bool skew_mode = argc > 4 && std::string(argv[4]) == "skew";
     const size_t bytes = mib << 20;
     const uint64_t nvec = bytes / 16;
     std::vector<Variant> vs;
@@ -331,6 +387,15 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 8; i++) rc.in[i] = reinterpret_cast<char*>(big) + i * bytes;
     const double b = (double)bytes;
 
+    if (skew_mode) {  // the multi-stream read penalty vs per-input offsets
+        add_readk<8>(vs, r, out, b, "");
+        add_readk<2>(vs, r, out, b, "");
+        for (uint64_t sk : {1ull, 64ull, 256ull, 1024ull, 1024ull * 7 + 1, 65536ull * 3 + 17})
+            add_skew<8>(vs, r, out, b, sk, false);
+        add_fan(vs, r, 8, b, "");
+        for (uint64_t sk : {0ull, 1024ull, 1024ull * 7 + 1, 65536ull * 3 + 17}) add_skew<8>(vs, r, out, b, sk, true);
+        return run(vs, s, rounds, reps, mib);
+    }
     if (pipe_mode) {
         add_fan(vs, r, 8, b, "");
         for (unsigned g : {256u, 512u, 1024u, 2048u}) add_pipe<8, 1024>(vs, r, g, b);

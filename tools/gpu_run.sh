@@ -57,6 +57,8 @@ for step in "$@"; do
             python tools/pmc_burst.py "$OUT/pmc_burst.json" "$OUT/pmcburst" > "$OUT/pmc_burst.out" 2>&1 ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
+        fanskew)
+            run fanskew 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 skew ;;
         fanlayout)
             run fanlayout 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 layout ;;
         policy)
