@@ -170,10 +170,14 @@ def plan(n_total, es, rank, world, scaling):
     return hi.value - lo.value, lo.value, n_total * es
 
 
-def timed_steps(step, steps, warmup, stream, world):
+def timed_steps(step, steps, warmup, stream, world, probe=10):
     """W untimed steps, then exactly K steps bracketed by a barrier and a
-    device synchronize on both sides; every launch between a HIP event pair
-    on the launch stream.  Returns (wall s, mean launch ms, launch ms list)."""
+    device synchronize on both sides, issued back to back with one HIP event
+    pair around all of them on the launch stream: mean launch time = that
+    region / K (the kernels plus their dependent-launch gaps, ~2 us each; no
+    per-launch instrumentation inside the timed region).  Afterwards, outside
+    it, `probe` launches each between their own event pair give the spread.
+    Returns (wall s, mean launch ms, probe launch ms list)."""
     import torch
     import torch.distributed as dist
 
@@ -181,23 +185,29 @@ def timed_steps(step, steps, warmup, stream, world):
     for _ in range(warmup):
         _lib.check(step(), "mi_reduce")
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        ev[i][0].record(stream)
+    e0.record(stream)
+    for _ in range(steps):
         rc = step()
-        ev[i][1].record(stream)
         if rc:
             _lib.check(rc, "mi_reduce")
+    e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    return elapsed, statistics.mean(kern_ms), kern_ms
+    avg_ms = e0.elapsed_time(e1) / steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(probe)]
+    for a, b in ev:
+        a.record(stream)
+        _lib.check(step(), "mi_reduce")
+        b.record(stream)
+    torch.cuda.synchronize()
+    return elapsed, avg_ms, [a.elapsed_time(b) for a, b in ev]
 
 
 def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None):
@@ -377,10 +387,13 @@ def main():
                          "algorithmic_bytes_per_launch": traffic_per_launch,
                          "avg_kernel_ms": round(avg_kern_ms, 5), "avg_kernel_ms_max_rank": round(avg_kern_ms_max, 5),
                          "kernel_ms_min": round(min(kern_ms), 5),
+                         "kernel_ms_probe": [round(x, 5) for x in kern_ms],
                          "aggregate": {"achieved": round(agg_achieved, 1), "peak": HBM_PEAK_GBPS * world,
                                        "frac": round(agg_achieved / (HBM_PEAK_GBPS * world), 4),
                                        "note": "all ranks' algorithmic launch bytes / max-over-ranks mean launch time"},
-                         "timing": "hipEvent pair around each launch on the launch stream; mean over timed steps",
+                         "timing": "one hipEvent pair on the launch stream around the K back-to-back timed launches "
+                                   "(avg_kernel_ms = that time / K, inter-launch gaps included); kernel_ms_min/_probe: "
+                                   "10 launches each between their own event pair, after the timed region",
                          "traffic_source": traffic.get("source") if traffic else None},
             "cpu_baseline": cpu,
         }
