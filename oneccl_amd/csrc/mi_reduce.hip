@@ -858,19 +858,19 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
                 din[i] = buf;
             }
         }
-        void* dout = (slot_of[k] < 0) ? static_cast<char*>(out) + off * es : d->dbuf[s][slot_of[k]];
+        void* cdst = (slot_of[k] < 0) ? static_cast<char*>(out) + off * es : d->dbuf[s][slot_of[k]];
         // The tail-truncation split is defined on the whole array: only the
         // last chunk holds elements >= (count/16)*16, and chunk starts are
         // multiples of 16, so the per-chunk split computed inside
         // launch_reduce is the same split.
-        rc = launch_reduce(din, k, dout, n, dt, op, flags, st);
+        rc = launch_reduce(din, k, cdst, n, dt, op, flags, st);
         if (rc) return rc;
         if (slot_of[k] >= 0) {
             if (drained) {
                 MI_HIP(hipEventRecord(d->ready[s], st));
-                drain->push({static_cast<char*>(out) + off * es, dout, bytes, d->ready[s]});
+                drain->push({static_cast<char*>(out) + off * es, cdst, bytes, d->ready[s]});
             } else {
-                MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, dout, bytes, hipMemcpyDeviceToHost, st));
+                MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, cdst, bytes, hipMemcpyDeviceToHost, st));
             }
         }
     }
