@@ -170,6 +170,20 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count,
                     int dtype, int op, unsigned flags, int device,
                     mi_request_t* req);
 int mi_test(mi_request_t req, int* done);
+/* The cooperative split as a request: elements [0, head_count) are folded by
+ * `head_fold` (a host reduce with mi_host_reduce's signature and semantics,
+ * include/mi_host_reduce.h) on the calling thread's staging worker while the
+ * GPU folds [head_count, count) — so neither half waits on the caller's
+ * thread.  Ordered with the thread's other requests like a staged one.  The
+ * caller keeps head_count a multiple of 256 elements (the bf16 keep-precision
+ * count % 16 tail must stay whole in the GPU part); head_count 0 is
+ * mi_reduce_start.  Used by ccl_comp_reduce_start / _batch_reduce_start for
+ * host buckets above the dispatcher's threshold.                           */
+typedef int (*mi_host_fold_t)(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                              unsigned flags);
+int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                          unsigned flags, int device, size_t head_count, mi_host_fold_t head_fold,
+                          mi_request_t* req);
 /* Wait until every request this thread has started with mi_reduce_start has
  * finished.  The synchronous entry points do this themselves; a caller about
  * to touch an earlier request's operands on the CPU (the drop-in's host

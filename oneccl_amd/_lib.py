@@ -47,6 +47,8 @@ MI_API = [
     ("mi_convert_sync", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_int]),
     ("mi_reduce_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
                                 POINTER(c_void_p)]),
+    ("mi_reduce_split_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
+                                      c_size_t, c_void_p, POINTER(c_void_p)]),
     ("mi_test", c_int, [c_void_p, POINTER(c_int)]),
     ("mi_thread_sync", c_int, []),
     ("mi_wait", c_int, [c_void_p]),

@@ -597,6 +597,31 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
 }
 
+// The asynchronous entries' issue.  A host bucket above the threshold is
+// split as in the synchronous path (coop_fold), but its head is folded on
+// the thread's staging worker (mi_reduce_split_start), not on the calling
+// thread the asynchronous form exists to free; the share is the thread's
+// adapted one (or the configured one).  Past the worker cap, and for device
+// operands, the GPU takes the whole bucket.
+int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags,
+               mi_request_t* r) {
+    const HostMax m = mi_host_max();
+    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
+    if (kind != 0 && shard_devices().size() < 2) {
+        const int pk = kind == 1 ? 1 : 0;
+        double share = pk ? m.share_pinned : m.share;
+        if (share > 0 && (pk ? m.adapt_pinned : m.adapt) && t_split.share[pk] >= 0) share = t_split.share[pk];
+        const int limit = pk ? m.split_workers_pinned : m.split_workers;
+        if (share > 0 && !(limit > 0 && host_workers() > limit)) {
+            size_t s = (size_t)((double)count * share);
+            s -= s % 256;
+            if (s > 0 && s < count)
+                return mi_reduce_split_start(ins, k, out, count, dt, op, flags, mi_comp_device(), s, &mi_host_reduce, r);
+        }
+    }
+    return mi_reduce_start(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
+}
+
 // conversions take the same route: the CPU for small host arrays
 int convert_sync(const void* src, int sdt, void* dst, int ddt, size_t count, unsigned flags) {
     const void* ins[1] = {src};
@@ -879,8 +904,7 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
                     return ccl::status::success;
                 }
                 mi_request_t r = nullptr;
-                check(mi_reduce_start(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f,
-                                      mi_comp_device(), &r),
+                check(start_fold(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f, &r),
                       "mi_reduce_start");
                 q->r.push_back(r);
             }
@@ -918,7 +942,7 @@ ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<si
                               return;
                           }
                           mi_request_t r = nullptr;
-                          check(mi_reduce_start(ins, k, out, n, dt, op, f, mi_comp_device(), &r), "mi_reduce_start");
+                          check(start_fold(ins, k, out, n, dt, op, f, &r), "mi_reduce_start");
                           q->r.push_back(r);
                       });
     drop.q = nullptr;

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <pthread.h>
 #include <sched.h>
 #include <stdexcept>
 #include <string>
@@ -538,6 +539,34 @@ struct DevCtx {
 };
 
 // ---------------------------------------------------------------------------
+// where helper threads run
+// ---------------------------------------------------------------------------
+// A new thread inherits its creator's CPU affinity.  oneCCL pins each worker
+// thread to one core (CCL_WORKER_AFFINITY), so the staging worker and the
+// drain thread a worker creates would share that one core with it, and with
+// the cooperative split's CPU head: measured with pinned workers, the GPU
+// path then ran at half its rate and the split below one core
+// (profiles/round2_dispatch/workers_pinned_inherit.jsonl).  Helpers therefore
+// take the CPU set the library was loaded with (the process's, before any
+// worker pinned itself); MI_REDUCE_HELPER_AFFINITY=inherit keeps the
+// creator's.
+struct HelperCpus {
+    cpu_set_t mask;
+    bool use = false;
+    HelperCpus() {
+        CPU_ZERO(&mask);
+        const char* e = getenv("MI_REDUCE_HELPER_AFFINITY");
+        if (e && strcmp(e, "inherit") == 0) return;
+        use = sched_getaffinity(0, sizeof(mask), &mask) == 0 && CPU_COUNT(&mask) > 0;
+    }
+};
+const HelperCpus g_helper_cpus;  // at library load
+
+void helper_thread_affinity() {
+    if (g_helper_cpus.use) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), &g_helper_cpus.mask);
+}
+
+// ---------------------------------------------------------------------------
 // drain thread for staged results bound for pageable host memory
 // ---------------------------------------------------------------------------
 // A D2H copy into pageable memory blocks the thread that issues it until the
@@ -567,6 +596,7 @@ struct Drain {
         th = std::thread([this, device, s] { loop(device, s); });
     }
     void loop(int device, hipStream_t s) {
+        helper_thread_affinity();
         hipError_t e = hipSetDevice(device);
         for (;;) {
             Task t;
@@ -916,6 +946,10 @@ struct AsyncJob {
     int dt = 0, op = 0;
     unsigned flags = 0;
     int device = -1;
+    // cooperative split (mi_reduce_split_start): [0, head) by head_fold on
+    // the worker thread while the GPU folds [head, count)
+    size_t head = 0;
+    mi_host_fold_t head_fold = nullptr;
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
@@ -931,6 +965,9 @@ struct AsyncJob {
         for (hipEvent_t e : prior) (void)hipEventDestroy(e);  // a job that never ran
     }
 };
+
+int run_split(const AsyncJob& j);
+int split_job(const AsyncJob& j) { return run_split(j); }
 
 struct StageWorker {
     std::thread th;
@@ -968,6 +1005,7 @@ struct StageWorker {
         cv.wait(lk, [&] { return inflight == 0; });
     }
     void loop() {
+        helper_thread_affinity();
         for (;;) {
             std::shared_ptr<AsyncJob> j;
             {
@@ -984,7 +1022,8 @@ struct StageWorker {
                 (void)hipEventDestroy(e);
             }
             j->prior.clear();
-            if (!rc) rc = reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags, j->device);
+            if (!rc) rc = j->head_fold ? split_job(*j) : reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op,
+                                                                       j->flags, j->device);
             {
                 std::lock_guard<std::mutex> lk(j->mu);
                 j->rc = rc;
@@ -1013,6 +1052,25 @@ thread_local StageWorker t_stage;
 // This thread has started asynchronous requests that mi_thread_sync has not
 // yet waited for.
 thread_local bool t_async_issued = false;
+
+// A split job, on the staging worker: the GPU part is started from here (a
+// pageable one is staged by this thread's own worker, one level down), the
+// head is folded on this thread meanwhile, then the GPU part is waited for.
+int run_split(const AsyncJob& j) {
+    const size_t es = dtype_size(j.dt);
+    const void* tail_in[MI_MAX_INPUTS];
+    for (int i = 0; i < j.k; i++) tail_in[i] = static_cast<const char*>(j.inputs[i]) + j.head * es;
+    mi_request_t r = nullptr;
+    if (int rc = mi_reduce_start(tail_in, j.k, static_cast<char*>(j.out) + j.head * es, j.count - j.head, j.dt, j.op,
+                                 j.flags, j.device, &r))
+        return rc;
+    const int hrc = j.head_fold(j.inputs, j.k, j.out, j.head, j.dt, j.op, j.flags);
+    const int wrc = mi_wait(r);
+    (void)mi_request_free(r);
+    if (wrc) return wrc;
+    if (hrc) return fail(hrc, "host fold of the split's head");
+    return 0;
+}
 
 // Events behind the work the calling thread has queued on its own streams
 // (every device it used); streams that are already idle need none.
@@ -1306,6 +1364,44 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
             mi_request_free(r);
             return rc;
         }
+        *req = r;
+        return 0;
+    });
+}
+
+int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                          unsigned flags, int device, size_t head_count, mi_host_fold_t head_fold,
+                          mi_request_t* req) {
+    if (head_count == 0 || count == 0) return mi_reduce_start(inputs, k, out, count, dtype, op, flags, device, req);
+    return guarded([&]() -> int {
+        if (!req) return fail(MI_E_INVALID, "null request pointer");
+        *req = nullptr;
+        if (!inputs) return fail(MI_E_INVALID, "null input list");
+        if (!head_fold) return fail(MI_E_INVALID, "null head fold");
+        if (head_count >= count) return fail(MI_E_INVALID, "head_count must leave a GPU part");
+        if (!dtype_size(dtype)) return fail(MI_E_INVALID, "unknown datatype");
+        if (k < 1 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "input count out of range [1,16]");
+        if (!out) return fail(MI_E_INVALID, "null output");
+        for (int i = 0; i < k; i++)
+            if (!inputs[i]) return fail(MI_E_INVALID, "null input");
+        if (op < MI_OP_SUM || op > MI_OP_MAX)
+            return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
+        t_async_issued = true;
+        auto j = std::make_shared<AsyncJob>();
+        j->prior = record_prior();
+        for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
+        j->k = k;
+        j->out = out;
+        j->count = count;
+        j->dt = dtype;
+        j->op = op;
+        j->flags = flags;
+        j->device = device;
+        j->head = head_count;
+        j->head_fold = head_fold;
+        t_stage.submit(j);
+        mi_request* r = new mi_request();
+        r->job = j;
         *req = r;
         return 0;
     });

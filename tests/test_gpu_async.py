@@ -278,3 +278,88 @@ def test_staged_and_direct_requests_keep_submission_order(first):
         _lib.check(m.mi_request_free(r))
     assert_same(from_dev(td, d0), exp_d, FP32, "device operand")
     assert_same(h, exp_h, FP32, "pageable operand")
+
+
+def _host_fold_ptr():
+    """mi_host_reduce (the shim's CPU fold) as a C function pointer."""
+    return ctypes.cast(_lib.shim().mi_host_reduce, ctypes.c_void_p).value
+
+
+@pytest.mark.parametrize("where", ["pageable", "pinned", "device"])
+@pytest.mark.parametrize("dt,op,flags", [(FP32, 0, 0), (BF16, 0, 0x2), (6, 3, 0), (4, 1, 0)],
+                         ids=["f32-sum", "bf16-sum-rne", "i64-max", "i32-prod"])
+def test_split_start_same_bits(where, dt, op, flags):
+    """mi_reduce_split_start: [0, head) folded by the host fold on the
+    thread's staging worker while the GPU folds the rest; the same bits as
+    the oracle over the whole bucket, for host and device operands."""
+    import torch
+    m = _lib.mi()
+    es = np.dtype(oracle.NP_DTYPE[dt]).itemsize
+    n = (40 << 20) // es + 37
+    head = (n * 2 // 5) // 256 * 256
+    a = rand_array(dt, n, seed=31 + op, op=op)
+    b = rand_array(dt, n, seed=32 + op, op=op)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, op, 8)  # bf16: the avx512bf impl (RNE) = MI_F_BF16_RNE
+    if where == "device":
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+        torch.cuda.synchronize()
+    elif where == "pinned":
+        ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        tb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        pa, pb = ta.data_ptr(), tb.data_ptr()
+    else:
+        hb = b.copy()
+        pa, pb = a.ctypes.data, hb.ctypes.data
+    if where == "device":  # the host fold must never see device memory: the GPU takes it whole
+        head = 0
+    req = ctypes.c_void_p()
+    _lib.check(m.mi_reduce_split_start(_lib.void_ptr_array([pb, pa]), 2, pb, n, dt, op, flags, -1, head,
+                                       _host_fold_ptr(), ctypes.byref(req)))
+    _lib.check(m.mi_wait(req))
+    _lib.check(m.mi_request_free(req))
+    got = from_dev(tb, b) if where == "device" else (tb.numpy().view(exp.dtype) if where == "pinned" else hb)
+    assert_same(got, exp, dt, where)
+
+
+def test_split_start_keeps_submission_order():
+    """A split request, then a device-only request that reads its output,
+    then a synchronous call on the first one's output: each sees the one
+    before, whichever side (host head or GPU tail) wrote the elements."""
+    import torch
+    m = _lib.mi()
+    n = (48 << 20) // 4
+    head = (n // 2) // 256 * 256
+    a = rand_array(FP32, n, seed=41, specials=False)
+    h = rand_array(FP32, n, seed=42, specials=False)
+    d0 = rand_array(FP32, n, seed=43, specials=False)
+    td, pd = to_dev(d0)
+    torch.cuda.synchronize()
+    exp_h, exp_d = h.copy(), d0.copy()
+    r1, r2 = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.check(m.mi_reduce_split_start(_lib.void_ptr_array([h.ctypes.data, a.ctypes.data]), 2, h.ctypes.data, n,
+                                       FP32, 0, 0, -1, head, _host_fold_ptr(), ctypes.byref(r1)))
+    oracle.comp_reduce_mt(a, exp_h, FP32, 0, 8)
+    _lib.check(m.mi_reduce_start(_lib.void_ptr_array([pd, h.ctypes.data]), 2, pd, n, FP32, 0, 0, -1,
+                                 ctypes.byref(r2)))
+    oracle.comp_reduce_mt(exp_h, exp_d, FP32, 0, 8)
+    _lib.check(m.mi_reduce_sync(pd, h.ctypes.data, n, FP32, 0, 0, -1))
+    oracle.comp_reduce_mt(exp_d, exp_h, FP32, 0, 8)
+    for r in (r1, r2):
+        _lib.check(m.mi_wait(r))
+        _lib.check(m.mi_request_free(r))
+    assert_same(from_dev(td, d0), exp_d, FP32, "device request after the split")
+    assert_same(h, exp_h, FP32, "sync call after both")
+
+
+def test_split_start_argument_errors():
+    m = _lib.mi()
+    a = np.ones(4096, np.float32)
+    arr = _lib.void_ptr_array([a.ctypes.data, a.ctypes.data])
+    req = ctypes.c_void_p()
+    assert m.mi_reduce_split_start(arr, 2, a.ctypes.data, a.size, FP32, 0, 0, -1, 256, None, ctypes.byref(req)) < 0
+    assert m.mi_reduce_split_start(arr, 2, a.ctypes.data, a.size, FP32, 0, 0, -1, a.size, _host_fold_ptr(),
+                                   ctypes.byref(req)) < 0
+    assert m.mi_reduce_split_start(arr, 2, a.ctypes.data, a.size, FP32, 4, 0, -1, 256, _host_fold_ptr(),
+                                   ctypes.byref(req)) < 0

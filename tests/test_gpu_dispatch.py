@@ -269,3 +269,53 @@ def test_split_yields_to_concurrent_workers(limit, threshold):
         assert all(s < 0 for s in shares), shares
     else:
         assert all(0.1 <= s <= 0.9 for s in shares), shares
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+@pytest.mark.parametrize("batch", [False, True], ids=["reduce", "batch-keep-precision"])
+def test_async_entry_splits_large_host_buckets(kind, batch, threshold):
+    """ccl_comp_reduce_start / ccl_comp_batch_reduce_start on a host bucket
+    above the threshold: the head is folded on the thread's staging worker,
+    the tail on the GPU (mi_reduce_split_start).  Same bits as the
+    synchronous call; the bf16 keep-precision count % 16 tail stays in the
+    GPU part."""
+    import torch
+    threshold(1 << 20)
+    b_impl, f_impl = comp.impl_types()
+    if batch:
+        k, n = 4, (6 << 20) + 11
+        ins = [rand_array(BF16, n, seed=700 + j, specials=False) for j in range(k)]
+        packed = np.concatenate(ins)
+        offsets = [j * n for j in range(k)]
+        exp = ins[0].copy()
+        oracle.batch_reduce(packed, offsets, n, exp, BF16, 0, 1, int(b_impl), 0)
+        got = ins[0].copy()
+        if kind == "pinned":
+            tp = torch.from_numpy(packed.view(np.uint8).copy()).pin_memory()
+            tg = torch.from_numpy(got.view(np.uint8).copy()).pin_memory()
+            pp, pg = tp.data_ptr(), tg.data_ptr()
+        else:
+            pp, pg = packed.ctypes.data, got.ctypes.data
+        req = comp.comp_batch_reduce_start(pp, offsets, n, pg, comp.datatype.bfloat16, comp.reduction.sum, 1)
+        req.wait()
+        req.free()
+        res = tg.numpy().view(np.uint16) if kind == "pinned" else got
+        assert_same(res, exp, BF16)
+        return
+    n = (40 << 20) // 4 + 9
+    a = rand_array(FP32, n, seed=81, specials=False)
+    b = rand_array(FP32, n, seed=82, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    if kind == "pinned":
+        ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        tb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        pa, pb = ta.data_ptr(), tb.data_ptr()
+    else:
+        hb = b.copy()
+        pa, pb = a.ctypes.data, hb.ctypes.data
+    req = comp.comp_reduce_start(pa, n, pb, comp.datatype.float32, comp.reduction.sum)
+    req.wait()
+    req.free()
+    got = tb.numpy().view(np.float32) if kind == "pinned" else hb
+    assert_same(got, exp, FP32, kind)

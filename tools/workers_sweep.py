@@ -24,7 +24,7 @@ threads' adapted split shares, and the cgroup's CPU throttling and the
 process's thread count over the mode's rounds.  The inputs are 0x3F bytes (no
 denormals).
 
-  python tools/workers_sweep.py [--workers 1,2,4,8,16] [--mib 8,64] [--reps 10] [--pinned]
+  python tools/workers_sweep.py [--workers 1,2,4,8,16] [--mib 8,64] [--reps 10] [--pinned] [--pin]
 """
 from __future__ import annotations
 
@@ -77,7 +77,7 @@ def set_mode(mode):
     comp.env_reload()
 
 
-def run_point(modes, w, nbytes, reps, pinned, f32=9):
+def run_point(modes, w, nbytes, reps, pinned, pin=None, f32=9):
     import numpy as np
 
     import oracle
@@ -90,6 +90,8 @@ def run_point(modes, w, nbytes, reps, pinned, f32=9):
 
     def worker(i):
         try:
+            if pin:  # one core per worker, as oneCCL pins its workers (CCL_WORKER_AFFINITY)
+                os.sched_setaffinity(0, {pin[i % len(pin)]})
             a = np.full(nbytes, 0x3F, np.uint8)  # first touch on this thread
             b = np.full(nbytes, 0x3F, np.uint8)
             fa, fb = a.view(np.float32), b.view(np.float32)
@@ -151,7 +153,7 @@ def run_point(modes, w, nbytes, reps, pinned, f32=9):
     for mode in modes:
         rs = rates[mode]
         row = {"workers": w, "bucket_MiB_per_worker": nbytes >> 20, "memory": "pinned" if pinned else "pageable",
-               "mode": mode, "GiBps_per_round": [round(x, 2) for x in rs]}
+               "mode": mode, "workers_pinned_to_cores": bool(pin), "GiBps_per_round": [round(x, 2) for x in rs]}
         if rs:
             tail = rs[len(rs) // 2:]
             row.update(best_GiBps=round(max(rs), 2), steady_median_GiBps=round(statistics.median(tail), 2))
@@ -175,6 +177,7 @@ def main():
     ap.add_argument("--modes", default="oracle,host,split,default")
     ap.add_argument("--pinned", action="store_true", help="register each thread's buffers with the GPU")
     ap.add_argument("--segv-trace", action="store_true", help="native backtrace on SIGSEGV (tools/libsegv_trace.so)")
+    ap.add_argument("--pin", action="store_true", help="pin each worker thread to its own core, as oneCCL does")
     args = ap.parse_args()
     if args.segv_trace:  # before faulthandler, which restores it when Python finalizes
         import ctypes
@@ -185,7 +188,8 @@ def main():
                                "nproc": os.cpu_count()}}), flush=True)
     for mib in (int(x) for x in args.mib.split(",")):
         for w in (int(x) for x in args.workers.split(",")):
-            for row in run_point(modes, w, mib << 20, args.reps, args.pinned):
+            pin = sorted(os.sched_getaffinity(0))[::-1] if args.pin else None  # oneCCL takes the last cores
+            for row in run_point(modes, w, mib << 20, args.reps, args.pinned, pin):
                 print(json.dumps(row), flush=True)
     print(json.dumps({"done": True}), flush=True)
 
