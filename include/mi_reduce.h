@@ -184,6 +184,11 @@ typedef int (*mi_host_fold_t)(const void* const* inputs, int k, void* out, size_
 int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
                           unsigned flags, int device, size_t head_count, mi_host_fold_t head_fold,
                           mi_request_t* req);
+/* A finished split request's two durations, in seconds from its start: the
+ * head (folded in ~8 MiB chunks) and the GPU part (seen done between two
+ * chunks, or at the end).  What the caller needs to move its share toward
+ * the point where both finish together.  MI_E_INVALID for other requests. */
+int mi_request_split_times(mi_request_t req, double* head_s, double* tail_s);
 /* Wait until every request this thread has started with mi_reduce_start has
  * finished.  The synchronous entry points do this themselves; a caller about
  * to touch an earlier request's operands on the CPU (the drop-in's host

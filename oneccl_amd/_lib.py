@@ -49,6 +49,7 @@ MI_API = [
                                 POINTER(c_void_p)]),
     ("mi_reduce_split_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
                                       c_size_t, c_void_p, POINTER(c_void_p)]),
+    ("mi_request_split_times", c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
     ("mi_test", c_int, [c_void_p, POINTER(c_int)]),
     ("mi_thread_sync", c_int, []),
     ("mi_wait", c_int, [c_void_p]),

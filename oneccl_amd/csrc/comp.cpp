@@ -603,20 +603,54 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
 // thread the asynchronous form exists to free; the share is the thread's
 // adapted one (or the configured one).  Past the worker cap, and for device
 // operands, the GPU takes the whole bucket.
+struct SplitIssued {      // an adaptive split issued by start_fold, for the share update on completion
+    mi_request_t req = nullptr;
+    int kind = 0;            // 0: some operand pageable, 1: all pinned
+    size_t count = 0, head = 0;
+    bool settled = false;    // the share update is done (or not wanted)
+};
+
+// On the caller's thread, once its split request is done: move the thread's
+// share for that pointer kind halfway toward the balance point, as coop_fold
+// does; a thread's first split of a kind only warms up.
+void settle_split(SplitIssued& sp) {
+    if (!sp.req || sp.settled) return;
+    sp.settled = true;
+    double th = 0, tt = 0;
+    if (mi_request_split_times(sp.req, &th, &tt) != 0 || th <= 0 || tt <= 0) return;
+    if (t_split.calls[sp.kind]++ == 0) return;
+    const double r_cpu = (double)sp.head / th, r_gpu = (double)(sp.count - sp.head) / tt;
+    double& cur = t_split.share[sp.kind];
+    cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
+}
+
 int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags,
-               mi_request_t* r) {
+               mi_request_t* r, SplitIssued* sp = nullptr) {
     const HostMax m = mi_host_max();
     const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
     if (kind != 0 && shard_devices().size() < 2) {
         const int pk = kind == 1 ? 1 : 0;
         double share = pk ? m.share_pinned : m.share;
-        if (share > 0 && (pk ? m.adapt_pinned : m.adapt) && t_split.share[pk] >= 0) share = t_split.share[pk];
+        const bool adapt = share > 0 && (pk ? m.adapt_pinned : m.adapt);
+        if (adapt) {
+            if (t_split.share[pk] < 0) t_split.share[pk] = share;
+            share = t_split.share[pk];
+        }
         const int limit = pk ? m.split_workers_pinned : m.split_workers;
         if (share > 0 && !(limit > 0 && host_workers() > limit)) {
             size_t s = (size_t)((double)count * share);
             s -= s % 256;
-            if (s > 0 && s < count)
-                return mi_reduce_split_start(ins, k, out, count, dt, op, flags, mi_comp_device(), s, &mi_host_reduce, r);
+            if (s > 0 && s < count) {
+                const int rc =
+                    mi_reduce_split_start(ins, k, out, count, dt, op, flags, mi_comp_device(), s, &mi_host_reduce, r);
+                if (rc == 0 && adapt && sp && !sp->req) {
+                    sp->req = *r;
+                    sp->kind = pk;
+                    sp->count = count;
+                    sp->head = s;
+                }
+                return rc;
+            }
         }
     }
     return mi_reduce_start(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
@@ -873,6 +907,7 @@ const char* ccl_reduction_to_str(ccl::reduction type) { return mi_reduction_to_s
 // ---- asynchronous ccl_comp_reduce (include/mi_ccl_comp_async.hpp) --------
 struct ccl_comp_request {
     std::vector<mi_request_t> r;  // empty: completed inside start (empty, custom, fp16 no-op)
+    SplitIssued split;            // the first adaptive split among them, if any
 };
 
 ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
@@ -904,7 +939,7 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
                     return ccl::status::success;
                 }
                 mi_request_t r = nullptr;
-                check(start_fold(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f, &r),
+                check(start_fold(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f, &r, &q->split),
                       "mi_reduce_start");
                 q->r.push_back(r);
             }
@@ -942,7 +977,7 @@ ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<si
                               return;
                           }
                           mi_request_t r = nullptr;
-                          check(start_fold(ins, k, out, n, dt, op, f, &r), "mi_reduce_start");
+                          check(start_fold(ins, k, out, n, dt, op, f, &r, &q->split), "mi_reduce_start");
                           q->r.push_back(r);
                       });
     drop.q = nullptr;
@@ -957,12 +992,14 @@ bool ccl_comp_request_test(ccl_comp_request* req) {
         check(mi_test(r, &done), "mi_test");
         if (!done) return false;
     }
+    settle_split(req->split);
     return true;
 }
 
 void ccl_comp_request_wait(ccl_comp_request* req) {
     if (!req) MI_CCL_THROW("null request");
     for (mi_request_t r : req->r) check(mi_wait(r), "mi_wait");
+    settle_split(req->split);
 }
 
 // Waits first if the request is still pending: freeing must never leave a

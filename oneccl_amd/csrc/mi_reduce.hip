@@ -950,6 +950,7 @@ struct AsyncJob {
     // the worker thread while the GPU folds [head, count)
     size_t head = 0;
     mi_host_fold_t head_fold = nullptr;
+    double t_head = -1.0, t_tail = -1.0;  // seconds from the split's start (run_split)
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
@@ -966,8 +967,8 @@ struct AsyncJob {
     }
 };
 
-int run_split(const AsyncJob& j);
-int split_job(const AsyncJob& j) { return run_split(j); }
+int run_split(AsyncJob& j);
+int split_job(AsyncJob& j) { return run_split(j); }
 
 struct StageWorker {
     std::thread th;
@@ -1056,19 +1057,43 @@ thread_local bool t_async_issued = false;
 // A split job, on the staging worker: the GPU part is started from here (a
 // pageable one is staged by this thread's own worker, one level down), the
 // head is folded on this thread meanwhile, then the GPU part is waited for.
-int run_split(const AsyncJob& j) {
+// The head runs in ~8 MiB chunks (multiples of 256 elements, so none holds a
+// keep-precision truncated tail), polling the GPU part between them: both
+// parts' durations are known even when the GPU finishes first, and the
+// caller adapts its share from them (mi_request_split_times).
+double mono_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int run_split(AsyncJob& j) {
     const size_t es = dtype_size(j.dt);
     const void* tail_in[MI_MAX_INPUTS];
     for (int i = 0; i < j.k; i++) tail_in[i] = static_cast<const char*>(j.inputs[i]) + j.head * es;
     mi_request_t r = nullptr;
+    const double t0 = mono_s();
     if (int rc = mi_reduce_start(tail_in, j.k, static_cast<char*>(j.out) + j.head * es, j.count - j.head, j.dt, j.op,
                                  j.flags, j.device, &r))
         return rc;
-    const int hrc = j.head_fold(j.inputs, j.k, j.out, j.head, j.dt, j.op, j.flags);
+    size_t chunk = std::max<size_t>(256, ((size_t)8 << 20) / es);
+    chunk -= chunk % 256;
+    int hrc = 0;
+    double t_tail = -1.0;
+    for (size_t b = 0; b < j.head && hrc == 0; b += chunk) {
+        const void* hin[MI_MAX_INPUTS];
+        for (int i = 0; i < j.k; i++) hin[i] = static_cast<const char*>(j.inputs[i]) + b * es;
+        hrc = j.head_fold(hin, j.k, static_cast<char*>(j.out) + b * es, std::min(chunk, j.head - b), j.dt, j.op,
+                          j.flags);
+        int done = 0;
+        if (t_tail < 0 && mi_test(r, &done) == 0 && done) t_tail = mono_s() - t0;
+    }
+    const double t_head = mono_s() - t0;
     const int wrc = mi_wait(r);
+    if (t_tail < 0) t_tail = mono_s() - t0;
     (void)mi_request_free(r);
     if (wrc) return wrc;
     if (hrc) return fail(hrc, "host fold of the split's head");
+    j.t_head = t_head;  // published to the caller by the job's done flag (under its mutex)
+    j.t_tail = t_tail;
     return 0;
 }
 
@@ -1405,6 +1430,16 @@ int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t co
         *req = r;
         return 0;
     });
+}
+
+int mi_request_split_times(mi_request_t req, double* head_s, double* tail_s) {
+    if (!req || !head_s || !tail_s) return fail(MI_E_INVALID, "null argument");
+    if (!req->job || !req->job->head_fold) return fail(MI_E_INVALID, "not a split request");
+    std::lock_guard<std::mutex> lk(req->job->mu);
+    if (!req->job->done || req->job->rc || req->job->t_head < 0) return fail(MI_E_INVALID, "split not finished");
+    *head_s = req->job->t_head;
+    *tail_s = req->job->t_tail;
+    return 0;
 }
 
 int mi_test(mi_request_t req, int* done) {

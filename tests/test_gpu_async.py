@@ -318,6 +318,12 @@ def test_split_start_same_bits(where, dt, op, flags):
     _lib.check(m.mi_reduce_split_start(_lib.void_ptr_array([pb, pa]), 2, pb, n, dt, op, flags, -1, head,
                                        _host_fold_ptr(), ctypes.byref(req)))
     _lib.check(m.mi_wait(req))
+    th, tt = ctypes.c_double(), ctypes.c_double()
+    rc = m.mi_request_split_times(req, ctypes.byref(th), ctypes.byref(tt))
+    if head:
+        assert rc == 0 and th.value > 0 and tt.value > 0, (rc, th.value, tt.value)
+    else:
+        assert rc < 0  # not a split
     _lib.check(m.mi_request_free(req))
     got = from_dev(tb, b) if where == "device" else (tb.numpy().view(exp.dtype) if where == "pinned" else hb)
     assert_same(got, exp, dt, where)

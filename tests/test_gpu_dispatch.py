@@ -319,3 +319,41 @@ def test_async_entry_splits_large_host_buckets(kind, batch, threshold):
     req.free()
     got = tb.numpy().view(np.float32) if kind == "pinned" else hb
     assert_same(got, exp, FP32, kind)
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+def test_async_split_adapts_its_share(kind, threshold):
+    """Without CCL_COMP_HOST_SHARE*, each finished asynchronous split moves
+    the calling thread's share toward the balance point, from the two parts'
+    durations its worker measured (mi_request_split_times): the share leaves
+    its 0.45 start and stays within [0.1, 0.9], and every call keeps the
+    bits."""
+    import time
+
+    import torch
+    threshold(1 << 20)
+    time.sleep(0.06)
+    n = (48 << 20) // 4 + 13
+    a = rand_array(FP32, n, seed=95, specials=False)
+    b0 = rand_array(FP32, n, seed=96, specials=False)
+    exp = b0.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    if kind == "pinned":
+        ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        tb = torch.empty(n * 4, dtype=torch.uint8).pin_memory()
+        pa, pb, hb = ta.data_ptr(), tb.data_ptr(), tb.numpy().view(np.float32)
+    else:
+        hb = np.empty_like(b0)
+        pa, pb = a.ctypes.data, hb.ctypes.data
+    shares = []
+    for i in range(5):
+        hb[:] = b0
+        req = comp.comp_reduce_start(pa, n, pb, comp.datatype.float32, comp.reduction.sum)
+        while not req.test():
+            pass
+        req.free()
+        assert_same(hb, exp, FP32, f"{kind} call {i}")
+        shares.append(_split_share(kind == "pinned"))
+    assert all(0.1 <= s <= 0.9 for s in shares), shares
+    assert shares[0] == pytest.approx(0.45)  # the first split of a kind only warms up
+    assert any(abs(s - 0.45) > 1e-9 for s in shares[1:]), shares

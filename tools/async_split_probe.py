@@ -12,7 +12,7 @@ For each: GiB/s of bucket (best and median of --reps, start to wait) and the
 microseconds the caller spends inside start (what a schedule entry's start()
 would block its worker for).  Buffers are 0x3F bytes (no denormals).
 
-  python tools/async_split_probe.py [--mib 32,64,256,1024] [--reps 8]
+  python tools/async_split_probe.py [--mib 32,64,256,1024] [--reps 8] [--pin]
 """
 from __future__ import annotations
 
@@ -47,8 +47,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", default="32,64,256,1024")
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--pin", action="store_true", help="after loading the library, pin this thread to one core "
+                                                        "(a oneCCL worker under CCL_WORKER_AFFINITY)")
     args = ap.parse_args()
-    from oneccl_amd import comp
+    from oneccl_amd import _lib, comp
+    _lib.mi()
+    _lib.shim()
+    if args.pin:
+        os.sched_setaffinity(0, {max(os.sched_getaffinity(0))})
     for mib in (int(x) for x in args.mib.split(",")):
         nbytes = mib << 20
         n = nbytes // 4
@@ -77,7 +83,7 @@ def main():
                         res[mode][0].append(nbytes / dt / 2**30)
                         res[mode][1].append(t_start * 1e6)
             for mode, (rates, starts) in res.items():
-                print(json.dumps({"bucket_MiB": mib, "memory": kind, "mode": mode,
+                print(json.dumps({"bucket_MiB": mib, "memory": kind, "mode": mode, "caller_pinned": args.pin,
                                   "best_GiBps": round(max(rates), 2), "median_GiBps": round(statistics.median(rates), 2),
                                   "caller_blocked_us_median": round(statistics.median(starts), 1)}), flush=True)
             del keep
