@@ -261,6 +261,26 @@ int main() {
             for (size_t i = 0; i < m; i++)
                 okk = okk && hbufs[2 * e + 1][i] == std::fmax((float)((i + 2 * e) % 251), (float)((i + 2 * e + 1) % 251));
         EXPECT(okk, "async host max");
+        // a host bucket above the dispatcher's threshold (16 MiB): split, the
+        // head folded on the worker's helper thread while the GPU takes the tail
+        {
+            const size_t big = (40u << 20) / 4 + 7;
+            float* bx = static_cast<float*>(staging_alloc(big * 4));
+            float* by = static_cast<float*>(staging_alloc(big * 4));
+            for (size_t i = 0; i < big; i++) {
+                bx[i] = (float)(i % 89);
+                by[i] = 3.0f;
+            }
+            async_reduce_entry bigen{bx, by, big, f32, ccl::reduction::sum};
+            bigen.start();
+            size_t sp = 0;
+            while (bigen.status != complete && sp++ < 200000000) bigen.update();
+            bool okb = bigen.status == complete;
+            for (size_t i = 0; i < big && okb; i++) okb = by[i] == (float)(i % 89) + 3.0f;
+            EXPECT(okb, "async split of a large host bucket");
+            free(bx);
+            free(by);
+        }
         // empty reduce: complete at start (comp.cpp:132-134)
         async_reduce_entry z{hbufs[0], hbufs[1], 0, f32, ccl::reduction::sum};
         z.start();
