@@ -83,6 +83,12 @@ enum mi_dtype {
  * final fp32 -> bf16 conversion are truncated, as the scalar tail loop of
  * ccl_convert_fp32_to_bf16_arrays does (src/comp/bf16/bf16.cpp:145-148).   */
 #define MI_F_BF16_TAIL_TRUNC16 0x8u
+/* fp16 min/max as VMINPH/VMAXPH (avx512fp16 impl, src/comp/fp16/
+ * fp16_intrisics.cpp:30-35): a NaN accumulator (`inout`) is returned as
+ * stored, so a signalling NaN stays signalling; clear = the fp32 route of the
+ * f16c/avx512f impls, whose VCVTPH2PS quiets it.  The only bits in which the
+ * two impls differ (oracle/FP16_NATIVE_CHECK.json).                        */
+#define MI_F_FP16_NATIVE_MINMAX 0x10u
 
 /* Error codes (< 0). */
 #define MI_E_INVALID (-1)      /* bad dtype / op / k / NULL pointer      */

@@ -64,6 +64,7 @@ F_MINMAX_INOUT_FIRST = 0x1
 F_BF16_RNE = 0x2
 F_ACC_FP32 = 0x4
 F_BF16_TAIL_TRUNC16 = 0x8
+F_FP16_NATIVE_MINMAX = 0x10
 
 DTYPE_SIZE = {datatype.int8: 1, datatype.uint8: 1, datatype.int16: 2, datatype.uint16: 2, datatype.int32: 4,
               datatype.uint32: 4, datatype.int64: 8, datatype.uint64: 8, datatype.float16: 2,

@@ -277,11 +277,15 @@ unsigned bf16_flags(ccl_bf16_impl_type impl) {
     return 0u;
 }
 
-// fp16: f16c / avx512f / avx512fp16 all compute in (or exactly as) fp32 with
-// MINPS order and RNE (fp16_intrisics.hpp:204-248); any other impl computes
-// nothing (it falls through every branch) — reproduced by returning false.
+// fp16: f16c / avx512f compute in fp32 with MINPS order and RNE
+// (fp16_intrisics.hpp:95-148); avx512fp16 in native fp16 (:150-176), which
+// gives the same bits for sum and prod (fp32 has 24 >= 2*11+2 bits) and for
+// min/max returns a NaN inout as stored (MI_F_FP16_NATIVE_MINMAX), all proven
+// on every operand pair (oracle/FP16_NATIVE_CHECK.json).  Any other impl
+// computes nothing (it falls through every branch, :204-248) — reproduced by
+// returning false.
 bool fp16_flags(ccl_fp16_impl_type impl, unsigned* f) {
-    *f = MI_F_MINMAX_INOUT_FIRST;
+    *f = MI_F_MINMAX_INOUT_FIRST | (impl == ccl_fp16_avx512fp16 ? MI_F_FP16_NATIVE_MINMAX : 0u);
     return impl == ccl_fp16_f16c || impl == ccl_fp16_avx512f || impl == ccl_fp16_avx512fp16;
 }
 

@@ -381,7 +381,7 @@ unsigned canon(int dt, int op, unsigned f, int k) {
         case MI_FLOAT32:
         case MI_FLOAT64: return mm ? (f & MI_F_MINMAX_INOUT_FIRST) : 0u;
         case MI_FLOAT16: {
-            unsigned v = (mm ? (f & MI_F_MINMAX_INOUT_FIRST) : 0u) | (f & MI_F_ACC_FP32);
+            unsigned v = (mm ? (f & (MI_F_MINMAX_INOUT_FIRST | MI_F_FP16_NATIVE_MINMAX)) : 0u) | (f & MI_F_ACC_FP32);
             if (k <= 2) v &= ~MI_F_ACC_FP32;
             return v;
         }
@@ -416,6 +416,25 @@ int mi_host_supported(void) {
                                                                                                               : 0;
 }
 
+// VMINPH/VMAXPH return the selected operand as stored, where the fp32 route's
+// VCVTPH2PS quiets it; they differ only when the accumulator's start is a
+// NaN, which a min/max fold then returns (oracle/fp16_native_check.c).  The
+// start is kept per block before the fold, since `out` may be that input.
+static int fold_fp16_native(FoldFn fn, const void* const* inputs, int k, void* out, size_t count, unsigned v) {
+    uint16_t raw[kChunk];
+    for (size_t b = 0; b < count; b += kChunk) {
+        const size_t n = std::min<size_t>(kChunk, count - b);
+        memcpy(raw, static_cast<const uint16_t*>(inputs[0]) + b, n * 2);
+        const void* ins[MI_MAX_INPUTS];
+        for (int j = 0; j < k; j++) ins[j] = static_cast<const uint16_t*>(inputs[j]) + b;
+        uint16_t* o = static_cast<uint16_t*>(out) + b;
+        fn(ins, k, o, n, v);
+        for (size_t i = 0; i < n; i++)
+            if ((raw[i] & 0x7C00u) == 0x7C00u && (raw[i] & 0x03FFu)) o[i] = raw[i];
+    }
+    return 0;
+}
+
 int mi_host_reduce(const void* const* inputs, int k, void* out, size_t count, int dtype, int op, unsigned flags) {
     if (!dsize(dtype)) return MI_E_INVALID;
     if (op < MI_OP_SUM || op > MI_OP_MAX) return MI_E_INVALID;
@@ -428,6 +447,11 @@ int mi_host_reduce(const void* const* inputs, int k, void* out, size_t count, in
     if (k == 1 && !(v & MI_F_ACC_FP32)) {  // nothing to combine
         if (out != inputs[0]) memmove(out, inputs[0], count * dsize(dtype));
         return 0;
+    }
+    if (v & MI_F_FP16_NATIVE_MINMAX) {  // fp16 min/max as VMINPH/VMAXPH (avx512fp16 impl)
+        FoldFn fn = pick(dtype, op, v & ~MI_F_FP16_NATIVE_MINMAX);
+        if (!fn) return MI_E_UNSUPPORTED;
+        return fold_fp16_native(fn, inputs, k, out, count, v & ~MI_F_FP16_NATIVE_MINMAX);
     }
     FoldFn fn = pick(dtype, op, v);
     if (!fn) return MI_E_UNSUPPORTED;

@@ -131,7 +131,7 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
         case MI_FLOAT32:
         case MI_FLOAT64: return mm ? (f & V_INOUT_FIRST) : 0u;
         case MI_FLOAT16: {
-            unsigned v = (mm ? (f & V_INOUT_FIRST) : 0u) | (f & V_ACC_FP32);
+            unsigned v = (mm ? (f & (V_INOUT_FIRST | V_FP16_NATIVE)) : 0u) | (f & V_ACC_FP32);
             if (k <= 2) v &= ~V_ACC_FP32;  // one step: same single rounding
             return v;
         }
@@ -209,6 +209,7 @@ constexpr bool valid_v() {
     if constexpr (!Tr<Tag>::fp) return V == 0;
     if constexpr (!Tr<Tag>::lp) return V == 0 || (mm && V == V_INOUT_FIRST);
     if ((V & V_INOUT_FIRST) && !mm) return false;
+    if ((V & V_FP16_NATIVE) && !(std::is_same<Tag, fp16_tag>::value && mm)) return false;
     if constexpr (std::is_same<Tag, fp16_tag>::value) return (V & (V_BF16_RNE | V_TAIL_TRUNC)) == 0;
     if ((V & V_TAIL_TRUNC) && !((V & V_ACC_FP32) && (V & V_BF16_RNE))) return false;
     return true;
@@ -232,6 +233,7 @@ Kern pick_v(unsigned v) {
 #define MI_V(n) case n: return entry<Tag, OP, n##u>();
         MI_V(0) MI_V(1) MI_V(2) MI_V(3) MI_V(4) MI_V(5) MI_V(6) MI_V(7)
         MI_V(8) MI_V(9) MI_V(10) MI_V(11) MI_V(12) MI_V(13) MI_V(14) MI_V(15)
+        MI_V(16) MI_V(17) MI_V(20) MI_V(21)  // V_FP16_NATIVE: fp16 min/max only (valid_v)
 #undef MI_V
         default: return Kern();
     }

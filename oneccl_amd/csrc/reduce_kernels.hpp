@@ -34,6 +34,7 @@ enum : unsigned {
     V_BF16_RNE = 2u,     // bf16 rounding: VCVTNEPS2BF16 (else truncate)
     V_ACC_FP32 = 4u,     // lp fan-in accumulates in fp32, one rounding at the end
     V_TAIL_TRUNC = 8u,   // with ACC|RNE: elements >= trunc_from truncate at the end
+    V_FP16_NATIVE = 16u, // fp16 min/max as VMINPH/VMAXPH (avx512fp16): a NaN accumulator as stored
 };
 
 constexpr int kMaxInputs = 16;
@@ -254,6 +255,20 @@ __device__ __forceinline__ typename Tr<Tag>::S finish_fold(typename Tr<Tag>::C a
 }
 
 
+// The avx512fp16 impl's VMINPH/VMAXPH(in, inout) return the selected operand
+// as stored; the fp32 route's widening (VCVTPH2PS) has quieted it.  They
+// differ only for a signalling NaN, and only the accumulator's start can be
+// the NaN a fold returns (a min/max step takes `in` only when in < acc,
+// ordered), so the result is that start, as stored, whenever it is a NaN
+// (oracle/fp16_native_check.c proves this over all 2^32 operand pairs).
+template <typename Tag, int OP, unsigned V>
+__device__ __forceinline__ typename Tr<Tag>::S native_minmax(typename Tr<Tag>::S r, typename Tr<Tag>::S acc0) {
+    if constexpr (std::is_same<Tag, fp16_tag>::value && (V & V_FP16_NATIVE) && (OP == OP_MIN || OP == OP_MAX)) {
+        if (((uint32_t)acc0 & 0x7C00u) == 0x7C00u && ((uint32_t)acc0 & 0x03FFu)) return acc0;
+    }
+    return r;
+}
+
 template <int MEM>
 __device__ __forceinline__ u32x4 vload(const u32x4* p) {
     if constexpr (MEM & 1)
@@ -322,7 +337,10 @@ __device__ __forceinline__ u32x4 fold_vec(const u32x4 (&x)[KMAX], int k, uint64_
     }
     Pack<S> pr;
 #pragma unroll
-    for (int e = 0; e < N; e++) pr.e[e] = finish_fold<Tag, V, X>(acc[e], e0 + e, trunc_from);
+    for (int e = 0; e < N; e++) {
+        pr.e[e] = finish_fold<Tag, V, X>(acc[e], e0 + e, trunc_from);
+        if constexpr (X) pr.e[e] = native_minmax<Tag, OP, V>(pr.e[e], p0.e[e]);  // NaN rows take X
+    }
     return __builtin_bit_cast(u32x4, pr);
 }
 
@@ -439,9 +457,10 @@ template <typename Tag, int OP, unsigned V>
 __device__ __forceinline__ void reduce_elem(const KArgs& a, int k, uint64_t idx) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
-    C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
+    const S s0 = static_cast<const S*>(a.in[0])[idx];
+    C acc = widen<Tag>(s0);
     for (int i = 1; i < k; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = native_minmax<Tag, OP, V>(finish_fold<Tag, V>(acc, idx, a.trunc_from), s0);
 }
 
 // One tile row: U vectors per lane at v0, v0+B, ...  GUARD = last tile.
@@ -454,6 +473,8 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
 
     C acc[U][N];
     u32x4 cur[U];
+    constexpr bool kNative = std::is_same<Tag, fp16_tag>::value && (V & V_FP16_NATIVE) && (OP == OP_MIN || OP == OP_MAX);
+    u32x4 raw0[kNative ? U : 1];  // the accumulator's start as stored (native_minmax)
 
     const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[0]) + hb);
     const u32x4* p1 =
@@ -464,6 +485,7 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
         const uint64_t v = v0 + (uint64_t)j * B;
         if (!GUARD || v < a.nvec) {
             u32x4 r = vload<MEM>(p0 + v);
+            if constexpr (kNative) raw0[j] = r;
             Pack<S> p = __builtin_bit_cast(Pack<S>, r);
 #pragma unroll
             for (int e = 0; e < N; e++) acc[j][e] = widen<Tag>(p.e[e]);
@@ -521,6 +543,11 @@ __device__ __forceinline__ void reduce_tile(const KArgs& a, int k, uint64_t v0) 
 #pragma unroll
             for (int e = 0; e < N; e++)
                 p.e[e] = finish_fold<Tag, V>(acc[j][e], a.head + v * N + e, a.trunc_from);
+            if constexpr (kNative) {
+                const Pack<S> s0 = __builtin_bit_cast(Pack<S>, raw0[j]);
+#pragma unroll
+                for (int e = 0; e < N; e++) p.e[e] = native_minmax<Tag, OP, V>(p.e[e], s0.e[e]);
+            }
             vstore<MEM>(po + v, __builtin_bit_cast(u32x4, p));
         }
     }
@@ -581,9 +608,10 @@ template <typename Tag, int OP, unsigned V>
 __device__ __forceinline__ void reduce2_elem(const R2Args& a, uint64_t idx) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
-    C acc = widen<Tag>(static_cast<const S*>(a.acc)[idx]);
+    const S s0 = static_cast<const S*>(a.acc)[idx];
+    C acc = widen<Tag>(s0);
     acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in)[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = native_minmax<Tag, OP, V>(finish_fold<Tag, V>(acc, idx, a.trunc_from), s0);
 }
 
 // One tile (block `blk` of the operand set `a`): the body of reduce2_kernel,
@@ -683,10 +711,11 @@ template <typename Tag, int OP, unsigned V, int K>
 __device__ __forceinline__ void reducek_elem(const RKArgs& a, uint64_t idx) {
     using S = typename Tr<Tag>::S;
     using C = typename Tr<Tag>::C;
-    C acc = widen<Tag>(static_cast<const S*>(a.in[0])[idx]);
+    const S s0 = static_cast<const S*>(a.in[0])[idx];
+    C acc = widen<Tag>(s0);
 #pragma unroll
     for (int i = 1; i < K; i++) acc = step<Tag, OP, V>(widen<Tag>(static_cast<const S*>(a.in[i])[idx]), acc);
-    static_cast<S*>(a.out)[idx] = finish_fold<Tag, V>(acc, idx, a.trunc_from);
+    static_cast<S*>(a.out)[idx] = native_minmax<Tag, OP, V>(finish_fold<Tag, V>(acc, idx, a.trunc_from), s0);
 }
 
 template <typename Tag, int OP, unsigned V, int K, int U, int B>

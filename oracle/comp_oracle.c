@@ -214,11 +214,16 @@ static int orc_bf16_reduce(const void* in_buf, size_t n, void* inout_buf, int op
 /* ccl_fp16_reduce -> ccl_fp16_reduce_impl, src/comp/fp16/fp16.cpp:41-53,
  * fp16_intrisics.hpp:204-248: f16c (8-wide) and avx512f (16-wide) widen to
  * fp32, apply MINPS/MAXPS-order ops, round RNE.  avx512fp16 does native
- * fp16 arithmetic (:150-176): for +,* on fp16 operands an fp32 result
- * rounded once to fp16 is the correctly rounded fp16 result (fp32 has
- * 24 >= 2*11+2 bits, so no double-rounding error), and VMINPH/VMAXPH
- * select like MINPS/MAXPS, so it yields the same values.  Any other impl
- * type falls through and computes nothing (:214-247) — reproduced. */
+ * fp16 arithmetic (fp16_intrisics.cpp:23-41, hpp :150-176): for +,* on fp16
+ * operands an fp32 result rounded once to fp16 is the correctly rounded fp16
+ * result (fp32 has 24 >= 2*11+2 bits, so no double-rounding error), so sum
+ * and prod give the same bits.  VMINPH/VMAXPH select like MINPS/MAXPS but
+ * return the selected operand as stored, where the fp32 route's VCVTPH2PS has
+ * quieted it: with a NaN `inout` (always the one selected) a signalling NaN
+ * stays signalling.  Both proven on all 2^32 operand pairs against IEEE
+ * binary16 arithmetic (oracle/fp16_native_check.c, FP16_NATIVE_CHECK.json).
+ * Any other impl type falls through and computes nothing (:214-247) —
+ * reproduced. */
 static int orc_fp16_reduce(const void* in_buf, size_t n, void* inout_buf, int op,
                            int impl) {
     const uint16_t* a = (const uint16_t*)in_buf;
@@ -226,7 +231,9 @@ static int orc_fp16_reduce(const void* in_buf, size_t n, void* inout_buf, int op
     if (op < OP_SUM || op > OP_MAX) return -1;
     if (impl != ORC_FP16_F16C && impl != ORC_FP16_AVX512F && impl != ORC_FP16_AVX512FP16)
         return 0;
+    const int native_mm = impl == ORC_FP16_AVX512FP16 && (op == OP_MIN || op == OP_MAX);
     for (size_t i = 0; i < n; i++) {
+        if (native_mm && (b[i] & 0x7C00u) == 0x7C00u && (b[i] & 0x03FFu)) continue; /* NaN inout, as stored */
         float r = lp_apply(op, 1, orc_fp16_to_fp32(a[i]), orc_fp16_to_fp32(b[i]));
         b[i] = orc_fp32_to_fp16_rne(r);
     }

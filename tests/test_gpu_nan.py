@@ -18,7 +18,7 @@ import pytest
 
 import oracle
 from oneccl_amd import _lib
-from oneccl_amd.comp import F_ACC_FP32, F_BF16_RNE, F_MINMAX_INOUT_FIRST
+from oneccl_amd.comp import F_ACC_FP32, F_BF16_RNE, F_FP16_NATIVE_MINMAX, F_MINMAX_INOUT_FIRST
 from tests.util import BF16, FP16, assert_same, from_dev, to_dev
 
 pytestmark = pytest.mark.gpu
@@ -34,6 +34,9 @@ VARIANTS = [
      lambda ins, op: oracle.fanin(ins, BF16, op, bf16_impl=oracle.BF16_AVX512BF)),
     ("fp16", FP16, F_MINMAX_INOUT_FIRST,
      lambda ins, op: oracle.fanin(ins, FP16, op, fp16_impl=oracle.FP16_AVX512F)),
+    # CCL_FP16=avx512fp16: VMINPH/VMAXPH keep a NaN accumulator as stored
+    ("fp16-native", FP16, F_MINMAX_INOUT_FIRST | F_FP16_NATIVE_MINMAX,
+     lambda ins, op: oracle.fanin(ins, FP16, op, fp16_impl=oracle.FP16_AVX512FP16)),
     ("bf16-acc32-rne", BF16, F_ACC_FP32 | F_BF16_RNE | F_MINMAX_INOUT_FIRST,
      lambda ins, op: oracle.lp_fanin_acc_fp32(ins, BF16, op, True, True)),
     ("fp16-acc32", FP16, F_ACC_FP32 | F_MINMAX_INOUT_FIRST,

@@ -341,3 +341,34 @@ def test_host_fanin_out_aliasing(dt, alias):
     arr = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
     assert _lib.shim().mi_host_reduce(arr, k, out.ctypes.data, n, dt, 0, 0) == 0
     assert_same(out, exp, dt, f"alias={alias}")
+
+
+@pytest.mark.parametrize("op", [2, 3], ids=["min", "max"])
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_host_fp16_native_minmax_keeps_snan_inout(op, k):
+    """CCL_FP16=avx512fp16 (MI_F_FP16_NATIVE_MINMAX): VMINPH/VMAXPH return a
+    NaN accumulator as stored, a signalling one included; the fp32 route of
+    the other impls quiets it.  Against the oracle with each impl."""
+    from oneccl_amd.comp import F_FP16_NATIVE_MINMAX
+    n = 1031
+    rng = np.random.default_rng(5 + op + k)
+    ins = [rand_array(FP16, n, seed=700 + j) for j in range(k)]
+    snan = rng.choice(n, 64, replace=False)
+    ins[0][snan] = (0x7C01 + rng.integers(0, 0x1FF, 64)) | (rng.integers(0, 2, 64) << 15)  # signalling NaNs
+    for j in range(1, k):
+        ins[j][rng.choice(n, 32, replace=False)] = 0x7E00  # quiet NaNs in the other inputs
+    for impl, flags in ((oracle.FP16_AVX512F, F_MINMAX_INOUT_FIRST),
+                        (oracle.FP16_AVX512FP16, F_MINMAX_INOUT_FIRST | F_FP16_NATIVE_MINMAX)):
+        exp = ins[0].copy()
+        for j in range(1, k):
+            oracle.comp_reduce(ins[j], exp, FP16, op, oracle.BF16_AVX512BF, impl)
+        for inplace in (False, True):
+            bufs = [x.copy() for x in ins]
+            out = bufs[0] if inplace else np.zeros_like(ins[0])
+            arr = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+            assert _lib.shim().mi_host_reduce(arr, k, out.ctypes.data, n, FP16, op, flags) == 0
+            assert_same(out, exp, FP16, f"impl {impl} inplace {inplace}")
+        if impl == oracle.FP16_AVX512FP16:
+            assert np.array_equal(exp[snan], ins[0][snan])  # signalling, as stored
+        else:
+            assert np.array_equal(exp[snan], ins[0][snan] | 0x0200)  # quieted

@@ -204,3 +204,35 @@ def test_oracle_is_sanitizer_clean():
     r = subprocess.run([str(ROOT / "oracle" / "lib" / "selftest_asan")], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "selftest: ok" in r.stdout
+
+
+def test_fp16_native_check_committed():
+    """oracle/FP16_NATIVE_CHECK.json: on all 2^32 (in, inout) fp16 pairs the
+    fp32 route equals IEEE binary16 arithmetic for sum and prod; min/max differ
+    exactly on a signalling-NaN inout (65536 x 1022 pairs); the IEEE model
+    equals the AVX512_FP16 instructions (VADDPH/VMULPH/VMINPH/VMAXPH, run on
+    this container's CPU), and the oracle's avx512fp16 model equals both."""
+    d = json.loads((ROOT / "oracle" / "FP16_NATIVE_CHECK.json").read_text())
+    assert d["stride"] == 1
+    assert d["native_model_vs_avx512fp16_hardware"] is True  # pinned to the instructions themselves
+    for op in ("sum", "prod", "min", "max"):
+        assert d[f"{op}_checked"] == 1 << 32
+        assert d[f"{op}_route_vs_native_unexplained"] == 0
+        assert d[f"{op}_oracle_vs_native"] == 0
+        assert d[f"{op}_hardware_vs_native"] == 0
+    assert d["sum_route_vs_native_snan_inout"] == d["prod_route_vs_native_snan_inout"] == 0
+    assert d["min_route_vs_native_snan_inout"] == d["max_route_vs_native_snan_inout"] == 65536 * 1022
+
+
+def test_fp16_native_check_sample():
+    """The same program on a strided sample, rebuilt and run here."""
+    import subprocess
+    exe = ROOT / "oracle" / "lib" / "fp16_native_check"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), str(Path("lib") / "fp16_native_check")], check=True)
+    r = subprocess.run([str(exe), "65537", "4"], capture_output=True, text=True, timeout=300)
+    if r.returncode == 2:
+        pytest.skip("CPU lacks F16C")
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout)
+    assert all(d[f"{op}_oracle_vs_native"] == 0 for op in ("sum", "prod", "min", "max"))
