@@ -10,18 +10,29 @@ from pathlib import Path
 import numpy as np
 
 PATH = Path(__file__).resolve().parent / "golden" / "ref_vectors.npz"
+# the avx512fp16 impl's vectors (tests/golden/make_ref_vectors_fp16native.py):
+# the reference's native half-precision code, run on a CPU with AVX512_FP16
+PATH_FP16NATIVE = Path(__file__).resolve().parent / "golden" / "ref_vectors_fp16native.npz"
 BF16, FP16 = 11, 8
 
 _cache = None
 
 
 def load():
-    """(arrays, cases): arrays by key, and the case list from the metadata."""
+    """(arrays, cases): arrays by key, and the case list from the metadata,
+    over both fixtures (their shared inputs are the same arrays)."""
     global _cache
     if _cache is None:
-        z = np.load(PATH)
-        arrs = {k: z[k] for k in z.files}
-        _cache = (arrs, json.loads(str(arrs.pop("meta"))))
+        arrs, cases = {}, []
+        for path in (PATH, PATH_FP16NATIVE):
+            z = np.load(path)
+            part = {k: z[k] for k in z.files}
+            meta = json.loads(str(part.pop("meta")))
+            for k, v in part.items():
+                assert k not in arrs or np.array_equal(arrs[k], v), k
+                arrs[k] = v
+            cases += meta["cases"]
+        _cache = (arrs, {"cases": cases})
     return _cache
 
 

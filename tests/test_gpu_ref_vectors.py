@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from oneccl_amd import _lib, comp
-from oneccl_amd.comp import F_BF16_RNE, F_MINMAX_INOUT_FIRST
+from oneccl_amd.comp import F_BF16_RNE, F_FP16_NATIVE_MINMAX, F_MINMAX_INOUT_FIRST
 from tests import refvec
 from tests.util import assert_same, from_dev, to_dev
 
@@ -26,9 +26,18 @@ pytestmark = pytest.mark.gpu
 
 # ccl impl type -> kernel flags (oneccl_amd/csrc/comp.cpp bf16_flags / fp16_flags)
 BF16_FLAGS = {1: F_MINMAX_INOUT_FIRST, 2: F_MINMAX_INOUT_FIRST | F_BF16_RNE}
-FP16_FLAGS = {2: F_MINMAX_INOUT_FIRST, 3: F_MINMAX_INOUT_FIRST}
+FP16_FLAGS = {2: F_MINMAX_INOUT_FIRST, 3: F_MINMAX_INOUT_FIRST, 4: F_MINMAX_INOUT_FIRST | F_FP16_NATIVE_MINMAX}
 ENV_NAME = {(refvec.BF16, 1): ("CCL_BF16", "avx512f"), (refvec.BF16, 2): ("CCL_BF16", "avx512bf"),
-            (refvec.FP16, 2): ("CCL_FP16", "f16c"), (refvec.FP16, 3): ("CCL_FP16", "avx512f")}
+            (refvec.FP16, 2): ("CCL_FP16", "f16c"), (refvec.FP16, 3): ("CCL_FP16", "avx512f"),
+            (refvec.FP16, 4): ("CCL_FP16", "avx512fp16")}
+
+
+def _cpu_has_avx512fp16():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return "avx512_fp16" in f.read()
+    except OSError:
+        return False
 
 
 def _flags(dt, impl):
@@ -102,6 +111,8 @@ def test_dropin_under_ccl_env_matches_reference_code(where, impl_env):
     import torch
     impl_env("CCL_COMP_HOST_MAX_BYTES", "0" if where == "host_gpu" else str(32 << 20))
     for c in refvec.reduce_cases():
+        if (c["dtype"], c["impl"]) == (refvec.FP16, 4) and not _cpu_has_avx512fp16():
+            continue  # CCL_FP16=avx512fp16 is refused on a CPU without it, as in oneCCL (env.cpp:715-720)
         impl_env(*ENV_NAME[(c["dtype"], c["impl"])])
         if where.startswith("host"):
             a, b = c["a"].copy(), c["b"].copy()

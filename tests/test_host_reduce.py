@@ -105,8 +105,9 @@ def test_host_keep_precision_matches_batch_reduce(bimpl, k, n):
 
 @pytest.mark.parametrize("c", refvec.reduce_cases(), ids=lambda c: c["key"])
 def test_host_reduce_matches_reference_code(c):
-    flags = ({1: F_MINMAX_INOUT_FIRST, 2: F_MINMAX_INOUT_FIRST | F_BF16_RNE}[c["impl"]]
-             if c["dtype"] == BF16 else F_MINMAX_INOUT_FIRST)
+    from oneccl_amd.comp import F_FP16_NATIVE_MINMAX
+    flags = ({1: F_MINMAX_INOUT_FIRST, 2: F_MINMAX_INOUT_FIRST | F_BF16_RNE}[c["impl"]] if c["dtype"] == BF16
+             else F_MINMAX_INOUT_FIRST | (F_FP16_NATIVE_MINMAX if c["impl"] == 4 else 0))
     b = c["b"].copy()
     arr = _lib.void_ptr_array([b.ctypes.data, c["a"].ctypes.data])
     assert _lib.shim().mi_host_reduce(arr, 2, b.ctypes.data, c["count"], c["dtype"], c["op"], flags) == 0

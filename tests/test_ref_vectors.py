@@ -11,6 +11,7 @@ committed file, so the fixture cannot drift from what the reference computes.
 from __future__ import annotations
 
 import subprocess
+import json
 from pathlib import Path
 
 import numpy as np
@@ -67,10 +68,12 @@ def test_oracle_bf16_load_matches_reference_code():
 def test_fixture_covers_every_avx512_variant():
     cases = refvec.reduce_cases()
     seen = {(c["dtype"], c["impl"], c["op"]) for c in cases}
-    assert seen == {(dt, i, op) for dt, impls in ((refvec.BF16, (1, 2)), (refvec.FP16, (2, 3)))
+    assert seen == {(dt, i, op) for dt, impls in ((refvec.BF16, (1, 2)), (refvec.FP16, (2, 3, 4)))
                     for i in impls for op in range(4)}
-    counts = {c["count"] for c in cases}
+    counts = {c["count"] for c in cases if c["impl"] != 4 or c["dtype"] != refvec.FP16}
     assert counts == {2061, 16, 15, 1}  # odd 16- and 8-wide tails, one full vector, a lone element
+    native = {c["count"] for c in cases if c["impl"] == 4 and c["dtype"] == refvec.FP16}
+    assert native == {2061, 32, 31, 1}  # avx512fp16: 32-wide body, masked tails
 
 
 @pytest.mark.skipif(not REF.is_dir(), reason="reference tree absent (GPU box): the committed fixture is used")
@@ -89,3 +92,39 @@ def test_fixture_regenerates_from_reference_code():
         if k == "meta":
             continue
         assert v.dtype == committed[k].dtype and np.array_equal(v.view(np.uint8), committed[k].view(np.uint8)), k
+
+
+def _has_avx512fp16():
+    try:
+        return "avx512_fp16" in Path("/proc/cpuinfo").read_text()
+    except OSError:
+        return False
+
+
+@pytest.mark.skipif(not REF.is_dir() or not _has_avx512fp16(),
+                    reason="needs the reference tree and a CPU with AVX512_FP16 (the committed fixture is used)")
+def test_fp16native_fixture_regenerates_from_reference_code():
+    """The avx512fp16 vectors: rebuild oracle/_ref/libref_fp16native.so (clang++
+    over the reference's fp16_intrisics.cpp) and regenerate; identical."""
+    r = subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import importlib.util
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    spec = importlib.util.spec_from_file_location("mrvn", ROOT / "tests" / "golden" / "make_ref_vectors_fp16native.py")
+    mrvn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mrvn)
+    fresh = mrvn.generate()
+    z = np.load(refvec.PATH_FP16NATIVE)
+    for k, v in fresh.items():
+        if k == "meta":
+            continue
+        assert v.dtype == z[k].dtype and np.array_equal(v.view(np.uint8), z[k].view(np.uint8)), k
+
+
+def test_fp16native_reference_code_exhaustive_result():
+    """oracle/FP16_NATIVE_REF_CHECK.json: the reference's own avx512fp16 code
+    against the oracle's model on all 2^32 (in, inout) pairs, every op."""
+    d = json.loads((ROOT / "oracle" / "FP16_NATIVE_REF_CHECK.json").read_text())
+    assert d["pairs_per_op"] == 1 << 32
+    assert all(d["mismatches"][op] == 0 for op in ("sum", "prod", "min", "max"))
