@@ -87,6 +87,10 @@ double mi_ccl_comp_split_share(int pinned);
  * threshold is split with the GPU only while this is at most
  * CCL_COMP_HOST_SPLIT_WORKERS (pageable) / _PINNED.  Diagnostic. */
 int mi_ccl_comp_host_workers(void);
+/* The calling thread's GPU-alone rate for host buckets of that pointer kind
+ * (elements/s; < 0 before it was timed) and how many buckets it will still
+ * run on the GPU alone (after a split lost to it, or as a probe).  Diagnostic. */
+double mi_ccl_comp_split_gpu_rate(int pinned, unsigned* gpu_left);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

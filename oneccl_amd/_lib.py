@@ -103,6 +103,7 @@ SHIM_API = [
     ("mi_ccl_env_reload", c_int, []),
     ("mi_ccl_comp_split_share", c_double, [c_int]),
     ("mi_ccl_comp_host_workers", c_int, []),
+    ("mi_ccl_comp_split_gpu_rate", c_double, [c_int, POINTER(c_uint)]),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

@@ -472,11 +472,45 @@ int host_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
 // (profiles/round2_dispatch/adapt_trace.jsonl).  The
 // chunks are multiples of 256 elements: each is a whole head region for the
 // keep-precision tail rule, as above.
+//
+// The share only balances the two parts' finishing times; whether splitting
+// pays at all is measured too.  Where a core reads the buffers slowly and its
+// head slows the GPU's zero-copy reads (hipHostMalloc'd pages on a far NUMA
+// node), the split ran up to 25 % below the GPU alone.  So an
+// adapting thread times the GPU alone now and then (its 3rd call of a kind,
+// then every 32nd split), and when a split's whole rate falls below 0.95 of
+// that, the next 8 buckets of that kind go to the GPU alone before a split
+// is tried again.
 struct SplitShare {
     double share[2] = {-1.0, -1.0};  // [0] some operand pageable, [1] all pinned; < 0: not started
     unsigned calls[2] = {0, 0};
+    double gpu_rate[2] = {-1.0, -1.0};  // elements / s of the whole bucket on the GPU alone
+    unsigned gpu_left[2] = {0, 0};      // buckets still to run on the GPU alone
+    unsigned since_probe[2] = {0, 0};   // split calls since the GPU alone was last timed
 };
 static thread_local SplitShare t_split;
+
+// After an adaptive split of `count` elements that took `t` seconds in all:
+// schedule GPU-alone calls (a probe, or a stretch when the split lost).
+static void split_verdict(int pk, size_t count, double t) {
+    SplitShare& sp = t_split;
+    const unsigned c = sp.calls[pk];
+    if (t > 0 && sp.gpu_rate[pk] > 0 && (double)count / t < 0.95 * sp.gpu_rate[pk]) {
+        sp.gpu_left[pk] = 8;
+        sp.since_probe[pk] = 0;
+    } else if (c == 2 || ++sp.since_probe[pk] >= 32) {
+        sp.gpu_left[pk] = 1;
+        sp.since_probe[pk] = 0;
+    }
+}
+
+// A bucket the GPU took alone in `t` seconds.
+static void gpu_alone_timed(int pk, size_t count, double t) {
+    if (t <= 0) return;
+    const double r = (double)count / t;
+    double& g = t_split.gpu_rate[pk];
+    g = g < 0 ? r : 0.5 * g + 0.5 * r;
+}
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -484,11 +518,19 @@ static double now_s() {
 
 int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags, double share,
               int pinned, bool adapt) {
-    double& cur = t_split.share[pinned ? 1 : 0];
-    unsigned& calls = t_split.calls[pinned ? 1 : 0];
+    const int pk = pinned ? 1 : 0;
+    double& cur = t_split.share[pk];
+    unsigned& calls = t_split.calls[pk];
     if (adapt) {
         if (cur < 0) cur = share;
         share = cur;
+        if (t_split.gpu_left[pk] > 0) {  // the GPU alone, timed
+            t_split.gpu_left[pk]--;
+            const double t0 = now_s();
+            const int rc = mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+            if (rc == 0) gpu_alone_timed(pk, count, now_s() - t0);
+            return rc;
+        }
     }
     const size_t es = mi_dtype_size(dt);
     size_t s = (size_t)((double)count * share);
@@ -520,6 +562,7 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     if (adapt && calls++ > 0 && hrc == 0 && wrc == 0 && t_cpu > 0 && t_gpu > 0) {
         const double r_cpu = (double)s / t_cpu, r_gpu = (double)(count - s) / t_gpu;
         cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
+        split_verdict(pk, count, std::max(t_cpu, t_gpu));
     }
     return wrc ? wrc : hrc;
 }
@@ -610,7 +653,8 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
 struct SplitIssued {      // an adaptive split issued by start_fold, for the share update on completion
     mi_request_t req = nullptr;
     int kind = 0;            // 0: some operand pageable, 1: all pinned
-    size_t count = 0, head = 0;
+    size_t count = 0, head = 0;  // head 0: a timed GPU-alone bucket
+    double t_start = 0;      // GPU-alone buckets: when it was issued
     bool settled = false;    // the share update is done (or not wanted)
 };
 
@@ -620,12 +664,17 @@ struct SplitIssued {      // an adaptive split issued by start_fold, for the sha
 void settle_split(SplitIssued& sp) {
     if (!sp.req || sp.settled) return;
     sp.settled = true;
+    if (sp.head == 0) {  // a GPU-alone bucket: its time as the caller saw it complete
+        gpu_alone_timed(sp.kind, sp.count, now_s() - sp.t_start);
+        return;
+    }
     double th = 0, tt = 0;
     if (mi_request_split_times(sp.req, &th, &tt) != 0 || th <= 0 || tt <= 0) return;
     if (t_split.calls[sp.kind]++ == 0) return;
     const double r_cpu = (double)sp.head / th, r_gpu = (double)(sp.count - sp.head) / tt;
     double& cur = t_split.share[sp.kind];
     cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
+    split_verdict(sp.kind, sp.count, std::max(th, tt));
 }
 
 int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags,
@@ -641,6 +690,19 @@ int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, i
             share = t_split.share[pk];
         }
         const int limit = pk ? m.split_workers_pinned : m.split_workers;
+        if (adapt && t_split.gpu_left[pk] > 0 && sp && !sp->req) {  // the GPU alone, timed to completion
+            t_split.gpu_left[pk]--;
+            const double t0 = now_s();
+            const int rc = mi_reduce_start(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
+            if (rc == 0) {
+                sp->req = *r;
+                sp->kind = pk;
+                sp->count = count;
+                sp->head = 0;
+                sp->t_start = t0;
+            }
+            return rc;
+        }
         if (share > 0 && !(limit > 0 && host_workers() > limit)) {
             size_t s = (size_t)((double)count * share);
             s -= s % 256;
@@ -1174,6 +1236,11 @@ int mi_ccl_env_reload(void) {
 double mi_ccl_comp_split_share(int pinned) { return t_split.share[pinned ? 1 : 0]; }
 
 int mi_ccl_comp_host_workers(void) { return host_workers(); }
+
+double mi_ccl_comp_split_gpu_rate(int pinned, unsigned* gpu_left) {
+    if (gpu_left) *gpu_left = t_split.gpu_left[pinned ? 1 : 0];
+    return t_split.gpu_rate[pinned ? 1 : 0];
+}
 
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl) {
     MI_SHIM_GUARD({

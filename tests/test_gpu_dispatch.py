@@ -5,6 +5,7 @@ the threshold give the reference's bits; a host-path call after an
 asynchronous GPU request of the same thread sees that request's result."""
 from __future__ import annotations
 
+import ctypes
 import os
 import subprocess
 from pathlib import Path
@@ -207,6 +208,10 @@ def test_adaptive_split_keeps_bits_and_bounds_its_share(kind, dt, threshold):
         shares.append(_split_share(kind == "pinned"))
     assert all(0.1 <= s <= 0.9 for s in shares), shares
     assert _split_share(kind != "pinned") < 0  # the other pointer kind's share is its own
+    # the 3rd call ran on the GPU alone, timed: whether splitting pays is measured too
+    from oneccl_amd import _lib
+    left = ctypes.c_uint(0)
+    assert _lib.shim().mi_ccl_comp_split_gpu_rate(1 if kind == "pinned" else 0, ctypes.byref(left)) > 0
 
 
 @pytest.mark.parametrize("env", [{"CCL_COMP_HOST_SHARE": "0.45", "CCL_COMP_HOST_SHARE_PINNED": "0.45"},
@@ -357,3 +362,6 @@ def test_async_split_adapts_its_share(kind, threshold):
     assert all(0.1 <= s <= 0.9 for s in shares), shares
     assert shares[0] == pytest.approx(0.45)  # the first split of a kind only warms up
     assert any(abs(s - 0.45) > 1e-9 for s in shares[1:]), shares
+    from oneccl_amd import _lib
+    left = ctypes.c_uint(0)
+    assert _lib.shim().mi_ccl_comp_split_gpu_rate(1 if kind == "pinned" else 0, ctypes.byref(left)) > 0
