@@ -8,6 +8,7 @@ oneccl_amd/lib/ and travel with the repo snapshot to the GPU box).
   tools/reduce_sweep  hipcc: launch-geometry / load-policy sweep (bench tool)
   tools/policy_sweep  hipcc: cache-policy / store-form / grid-stride experiment
   tools/fan_sweep     hipcc: fan-in input order experiment
+  tools/copy_sweep    hipcc: shapes of the device copy (ccl_comp_copy)
 """
 from __future__ import annotations
 
@@ -117,6 +118,14 @@ def build_burst_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_copy_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "copy_sweep"
+    src = ROOT / "tools" / "copy_sweep.hip"
+    if src.exists() and (force or _stale(out, [src, CSRC / "reduce_kernels.hpp"])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
 def build_latency(force: bool = False) -> Path:
     out = ROOT / "tools" / "latency"
     src = ROOT / "tools" / "latency.hip"
@@ -207,6 +216,7 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_policy_sweep()
     build_fan_sweep()
     build_burst_sweep()
+    build_copy_sweep()
     build_latency()
     build_segv_trace()
     if asan:

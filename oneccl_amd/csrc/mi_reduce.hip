@@ -1586,17 +1586,29 @@ int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* str
     const uint32_t head = (uint32_t)std::min<size_t>((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u, bytes);
     const uint64_t nvec = (bytes - head) / 16;
     const uint32_t tail = (uint32_t)(bytes - head - nvec * 16);
-    const uint64_t tile = (uint64_t)kBlock * 4;
-    uint64_t blocks = (nvec + tile - 1) / tile;
-    const int cap = max_blocks();
-    if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
-    blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 0x7FFFFFFFull);
     const char* s8 = static_cast<const char*>(src);
     char* d8 = static_cast<char*>(dst);
+    // loads are non-temporal either way (each byte is read once); `nontemporal`
+    // picks the stores, as the reference's flag picks its memcpy
+    const int cap = max_blocks();
+    const uint64_t lean_blocks = (nvec + kCopyBlock - 1) / kCopyBlock;
+    if (cap <= 0 && lean_blocks <= 0x7FFFFFFFull) {
+        const unsigned blocks = (unsigned)std::max<uint64_t>(lean_blocks, 1);
+        if (nontemporal)
+            hipLaunchKernelGGL(copy_lean_kernel<3>, dim3(blocks), dim3(kCopyBlock), 0, s, s8, d8, head, nvec, tail);
+        else
+            hipLaunchKernelGGL(copy_lean_kernel<1>, dim3(blocks), dim3(kCopyBlock), 0, s, s8, d8, head, nvec, tail);
+        MI_HIP(hipGetLastError());
+        return 0;
+    }
+    const uint64_t tile = (uint64_t)kBlock * 4;
+    uint64_t blocks = (nvec + tile - 1) / tile;
+    if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
+    blocks = std::min<uint64_t>(std::max<uint64_t>(blocks, 1), 0x7FFFFFFFull);
     if (nontemporal)
-        hipLaunchKernelGGL(copy_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
+        hipLaunchKernelGGL(copy_kernel<3>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
     else
-        hipLaunchKernelGGL(copy_kernel<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
+        hipLaunchKernelGGL(copy_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, s, s8, d8, head, nvec, tail);
     MI_HIP(hipGetLastError());
     return 0;
 }

@@ -260,23 +260,30 @@ def test_custom_reduction_callback():
     assert b"callback" in _lib.shim().mi_ccl_last_error()
 
 
+@pytest.mark.parametrize("cap", [0, 3], ids=["lean", "capped"])
 @pytest.mark.parametrize("nt", [0, 1])
-def test_comp_copy_any_offsets(nt):
+def test_comp_copy_any_offsets(nt, cap):
     """ccl_comp_copy between device buffers at every byte offset pair mod 16
-    and odd sizes: the copy kernel on the destination's 16-byte grid."""
+    and odd sizes: the copy kernel on the destination's 16-byte grid, as the
+    one-tile-per-block kernel (default) and the grid-stride one (a grid cap)."""
     import torch
+    m = _lib.mi()
     rng = np.random.default_rng(5)
     src = torch.from_numpy(rng.integers(0, 256, 1 << 20, dtype=np.uint8)).cuda()
     ref = src.cpu().numpy()
-    for so in (0, 1, 3, 4, 8, 15):
-        for do in (0, 2, 5, 12):
-            for n in (1, 15, 16, 17, 4099, (1 << 19) + 3):
-                dst = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
-                torch.cuda.synchronize()  # the fill runs on torch's stream, the copy on the library's
-                comp.comp_copy(src.data_ptr() + so, dst.data_ptr() + do, n, bool(nt))
-                got = dst.cpu().numpy()
-                assert np.array_equal(got[do:do + n], ref[so:so + n]), (so, do, n)
-                assert not got[:do].any() and not got[do + n:].any(), (so, do, n)
+    _lib.check(m.mi_set_max_blocks(cap))
+    try:
+        for so in (0, 1, 3, 4, 8, 15):
+            for do in (0, 2, 5, 12):
+                for n in (1, 15, 16, 17, 8191, 8193, 4099, (1 << 19) + 3):
+                    dst = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+                    torch.cuda.synchronize()  # the fill runs on torch's stream, the copy on the library's
+                    comp.comp_copy(src.data_ptr() + so, dst.data_ptr() + do, n, bool(nt))
+                    got = dst.cpu().numpy()
+                    assert np.array_equal(got[do:do + n], ref[so:so + n]), (so, do, n)
+                    assert not got[:do].any() and not got[do + n:].any(), (so, do, n)
+    finally:
+        _lib.check(m.mi_set_max_blocks(0))
 
 
 @pytest.mark.parametrize("nt", [0, 1])

@@ -57,6 +57,14 @@ for step in "$@"; do
             python tools/pmc_burst.py "$OUT/pmc_burst.json" "$OUT/pmcburst" > "$OUT/pmc_burst.out" 2>&1 ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
+        copysweep)
+            run copysweep 300 ./tools/copy_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
+        copyprof)  # per-kernel durations of every copy_sweep variant
+            (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$GRAFT_REPO_ROOT/$OUT/copyprof" -o copy -- "$GRAFT_REPO_ROOT/tools/copy_sweep" 1024 2 8 \
+                > "$GRAFT_REPO_ROOT/$OUT/copyprof.out" 2> "$GRAFT_REPO_ROOT/$OUT/copyprof.err")
+            rc=$?; echo "=== copyprof rc=$rc" | tee -a "$OUT/steps.log"
+            [ $rc -eq 0 ] || exit $rc ;;
         fanskew)
             run fanskew 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 skew ;;
         fanlayout)
