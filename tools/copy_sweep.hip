@@ -4,7 +4,9 @@
 // hipMemcpy D2D, interleaved in one process on a 1 GiB buffer.  Also each shape with the
 // source 4 bytes off the destination's 16-byte grid (mi_copy's unaligned-source
 // case).  Traffic = 2 bytes per byte copied.
-//   copy_sweep [MiB=1024] [rounds=5] [reps=10]
+// Then the conversion kernel (fp32 <-> bf16 / fp16 arrays, 6 bytes per element)
+// at three block sizes, unless the 4th argument is "nocvt".
+//   copy_sweep [MiB=1024] [rounds=5] [reps=10] [nocvt]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -67,7 +69,28 @@ struct Variant {
     std::string name;
     std::function<void(hipStream_t)> run;
     std::vector<float> ms;
+    double traffic = 0;  // bytes per launch; 0 = 2 x the buffer (a copy)
 };
+
+// the library's conversion kernel (ccl_convert_*_arrays) at block size B:
+// `count` elements, both buffers 16-byte aligned
+template <typename ST, typename DT, unsigned V, int B>
+void add_convert(std::vector<Variant>& vs, const char* label, const void* src, void* dst, uint64_t count) {
+    CArgs a{};
+    a.src = src;
+    a.dst = dst;
+    a.count = count;
+    a.head = 0;
+    a.ngroups = count / 8;
+    a.trunc_from = count;
+    a.scalar_only = 0;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((a.ngroups + B - 1) / B, 1u << 20);
+    const double t = (double)count * (sizeof(typename Tr<ST>::S) + sizeof(typename Tr<DT>::S));
+    vs.push_back({std::string("convert ") + label + " B=" + std::to_string(B) + (B == kBlock ? " (library)" : ""),
+                  [a, blocks](hipStream_t st) {
+                      hipLaunchKernelGGL((convert_kernel<ST, DT, V, B>), dim3(blocks), dim3(B), 0, st, a);
+                  }, {}, t});
+}
 
 int main(int argc, char** argv) {
     const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
@@ -143,6 +166,20 @@ int main(int argc, char** argv) {
                       [=](hipStream_t st) { (void)hipMemcpyAsync(dst, sp, bytes, hipMemcpyDeviceToDevice, st); }, {}});
     }
 
+    if (!(argc > 4 && std::string(argv[4]) == "nocvt")) {
+        const uint64_t count = bytes / 4;  // fp32 side = the buffer, 16-bit side = half of it
+        add_convert<float, bf16_tag, V_BF16_RNE, 256>(vs, "fp32->bf16 RNE", src, dst, count);
+        add_convert<float, bf16_tag, V_BF16_RNE, 512>(vs, "fp32->bf16 RNE", src, dst, count);
+        add_convert<float, bf16_tag, V_BF16_RNE, 1024>(vs, "fp32->bf16 RNE", src, dst, count);
+        add_convert<bf16_tag, float, 0u, 256>(vs, "bf16->fp32", src, dst, count);
+        add_convert<bf16_tag, float, 0u, 512>(vs, "bf16->fp32", src, dst, count);
+        add_convert<bf16_tag, float, 0u, 1024>(vs, "bf16->fp32", src, dst, count);
+        add_convert<float, fp16_tag, 0u, 256>(vs, "fp32->fp16", src, dst, count);
+        add_convert<float, fp16_tag, 0u, 1024>(vs, "fp32->fp16", src, dst, count);
+        add_convert<fp16_tag, float, 0u, 256>(vs, "fp16->fp32", src, dst, count);
+        add_convert<fp16_tag, float, 0u, 1024>(vs, "fp16->fp32", src, dst, count);
+    }
+
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -162,8 +199,8 @@ int main(int argc, char** argv) {
         }
         fprintf(stderr, "round %d/%d done\n", r + 1, rounds);
     }
-    const double traffic = 2.0 * bytes;
     for (auto& v : vs) {
+        const double traffic = v.traffic > 0 ? v.traffic : 2.0 * bytes;
         std::sort(v.ms.begin(), v.ms.end());
         const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
         printf("{\"variant\": \"%s\", \"MiB\": %zu, \"median_ms\": %.5f, \"best_ms\": %.5f, \"median_GBps\": %.1f, "
