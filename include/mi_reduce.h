@@ -313,7 +313,8 @@ int mi_device_count(void);
 /* Launch geometry the vector kernels use: threads per block, 16-byte
  * vectors per lane per tile, and the grid cap (0 = one tile per block).   */
 int mi_get_launch_config(int* block, int* unroll, int* max_blocks);
-/* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS). */
+/* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS).  Under a
+ * cap the reduce, copy and conversion kernels stride over the buffer.     */
 int mi_set_max_blocks(int max_blocks);
 
 #ifdef __cplusplus

@@ -1191,6 +1191,8 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     a.ngroups = vec ? (count - a.head) / 8 : 0;
     const uint64_t work = a.scalar_only ? count : std::max<uint64_t>(a.ngroups, 1);
     uint64_t blocks = std::min<uint64_t>((work + kBlock - 1) / kBlock, 1u << 20);
+    const int cap = max_blocks();  // a grid cap (mi_set_max_blocks) makes the kernel stride
+    if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
     blocks = std::max<uint64_t>(blocks, 1);
     hipError_t e = fn(dim3((unsigned)blocks), s, a);
     if (e != hipSuccess) return hip_fail(e, "convert kernel launch");

@@ -112,12 +112,15 @@ CONV_PAIRS = [(FP32, BF16, comp.F_BF16_RNE | comp.F_BF16_TAIL_TRUNC16), (FP32, B
 @pytest.mark.parametrize("sdt,ddt,flags", CONV_PAIRS, ids=["f32-bf16rne-tail", "f32-bf16trunc", "f32-f16",
                                                            "bf16-f32", "f16-f32"])
 @pytest.mark.parametrize("offs", [(0, 0), (1, 0), (0, 1), (3, 5), (2, 7)])
-@pytest.mark.parametrize("vectors", [1, 0], ids=["unaligned-vectors", "element-loop"])
-def test_convert_any_offsets(sdt, ddt, flags, offs, vectors):
+@pytest.mark.parametrize("vectors,cap", [(1, 0), (0, 0), (1, 3), (1, 5)],
+                         ids=["unaligned-vectors", "element-loop", "grid-cap-3", "grid-cap-5"])
+def test_convert_any_offsets(sdt, ddt, flags, offs, vectors, cap):
     """Conversions between sub-buffers at any element offsets: the vector path
     on dst's 16-byte grid (scalar head, unaligned source vectors, tail) and the
     element loop give the oracle's bits, including the count % 16 truncated
-    tail of ccl_convert_fp32_to_bf16_arrays (bf16.cpp:145-148)."""
+    tail of ccl_convert_fp32_to_bf16_arrays (bf16.cpp:145-148).  A grid cap
+    makes every lane stride through many 64-group wave chunks (two runs of 4
+    elements per lane) before the partial last chunk."""
     n = 8 * 4099 + 13
     rng = np.random.default_rng(sum(offs) + 10 * sdt + ddt)
     f = (rng.standard_normal(n) * 7).astype(np.float32)
@@ -136,10 +139,12 @@ def test_convert_any_offsets(sdt, ddt, flags, offs, vectors):
         out_dtype = np.float32
     m = _lib.mi()
     prev = m.mi_set_unaligned_vectors(vectors)
+    _lib.check(m.mi_set_max_blocks(cap))
     try:
         got = _gpu_convert(src, sdt, ddt, flags, out_dtype, *offs)
     finally:
         m.mi_set_unaligned_vectors(prev)
+        _lib.check(m.mi_set_max_blocks(0))
     assert_same(got, exp, ddt)
 
 
