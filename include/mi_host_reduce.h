@@ -32,6 +32,11 @@ int mi_host_supported(void);
 int mi_host_reduce(const void* const* inputs, int k, void* out, size_t count,
                    int dtype, int op, unsigned flags);
 
+/* Host-to-host copy (ccl_comp_copy, src/comp/comp.cpp:60-74).  nontemporal:
+ * streaming stores above 256 bytes, as the reference's memcpy_nontemporal
+ * (src/common/utils/memcpy.cpp:49-125); else a memcpy.  No overlap. */
+int mi_host_copy(void* dst, const void* src, size_t bytes, int nontemporal);
+
 /* fp32 <-> bf16 / fp16 array conversion, mi_convert's semantics. */
 int mi_host_convert(const void* src, int src_dtype, void* dst, int dst_dtype,
                     size_t count, unsigned flags);

@@ -114,6 +114,7 @@ HOST_API = [
     ("mi_host_supported", c_int, []),
     ("mi_host_reduce", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint]),
     ("mi_host_convert", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint]),
+    ("mi_host_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int]),
 ]
 
 

@@ -758,9 +758,10 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
     if (!in_buf) MI_CCL_THROW("in_buf is null");
     if (!out_buf) MI_CCL_THROW("out_buf is null");
     const void* src[1] = {in_buf};
-    if (mi_host_max().pageable > 0 && all_host(src, 1, out_buf)) {  // host to host: a memcpy, as the reference
+    if (mi_host_max().pageable > 0 && all_host(src, 1, out_buf)) {  // host to host on the CPU, as the reference
         check(mi_thread_sync(), "mi_thread_sync");
-        memcpy(out_buf, in_buf, bytes);
+        // (the host path is on only where mi_host_supported(): AVX2 is there)
+        check(mi_host_copy(out_buf, in_buf, bytes, use_nontemporal ? 1 : 0), "mi_host_copy");
         return ccl::status::success;
     }
     check(mi_copy_sync(in_buf, out_buf, bytes, use_nontemporal ? 1 : 0, mi_comp_device()), "mi_copy_sync");

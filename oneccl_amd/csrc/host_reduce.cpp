@@ -459,6 +459,42 @@ int mi_host_reduce(const void* const* inputs, int k, void* out, size_t count, in
     return 0;
 }
 
+// Host-to-host ccl_comp_copy (src/comp/comp.cpp:60-74).  With `nontemporal`
+// the destination is written with streaming stores from its first 64-byte
+// boundary on (no read-for-ownership of the destination lines, nothing left
+// in the caches), as the reference's memcpy_nontemporal does for copies above
+// 256 bytes (src/common/utils/memcpy.cpp:49-125); the bytes are the same
+// either way.  Unaligned 32-byte loads, 128 bytes per step.
+int mi_host_copy(void* dst, const void* src, size_t bytes, int nontemporal) {
+    if (bytes == 0) return 0;
+    if (!src || !dst) return MI_E_INVALID;
+    if (!nontemporal || bytes <= 256) {
+        memcpy(dst, src, bytes);
+        return 0;
+    }
+    char* d = static_cast<char*>(dst);
+    const char* s = static_cast<const char*>(src);
+    const size_t head = (64 - (reinterpret_cast<uintptr_t>(d) & 63)) & 63;
+    memcpy(d, s, head);
+    size_t i = head;
+    for (; i + 128 <= bytes; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+        const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+    }
+    for (; i + 32 <= bytes; i += 32)
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i),
+                            _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i)));
+    memcpy(d + i, s + i, bytes - i);
+    _mm_sfence();  // the streaming stores are visible before the caller sends the buffer
+    return 0;
+}
+
 int mi_host_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t count, unsigned flags) {
     if (count == 0) return 0;
     if (!src || !dst) return MI_E_INVALID;

@@ -212,6 +212,27 @@ def test_dropin_host_batch_reduce(keep, k, dt, env):
     assert oc == oc_ref
 
 
+@pytest.mark.parametrize("nt", [0, 1])
+def test_host_copy_offsets_and_sizes(nt):
+    """mi_host_copy (host-to-host ccl_comp_copy): with nontemporal, streaming
+    stores from the destination's first 64-byte boundary, 128 and 32 bytes per
+    step, memcpy head and tail (the reference's memcpy_nontemporal switches at
+    256 bytes, src/common/utils/memcpy.cpp:59).  Bytes equal at every offset
+    pair and size around those steps; nothing outside the range is written."""
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    hc = _lib.shim().mi_host_copy
+    for so in (0, 1, 7, 32, 63):
+        for do in (0, 1, 31, 32, 60):
+            for n in (1, 255, 256, 257, 300, 383, 4096 + 5, 60_000):
+                dst = np.zeros(n + 128, np.uint8)
+                assert hc(dst.ctypes.data + do, src.ctypes.data + so, n, nt) == 0
+                assert np.array_equal(dst[do:do + n], src[so:so + n]), (so, do, n)
+                assert not dst[:do].any() and not dst[do + n:].any(), (so, do, n)
+    assert hc(0, 0, 0, nt) == 0
+    assert hc(0, src.ctypes.data, 5, nt) < 0
+
+
 def test_dropin_host_conversions_and_copy():
     f = rand_array(FP32, 37, seed=3)
     b_impl, _ = comp.impl_types()
