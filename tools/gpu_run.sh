@@ -65,6 +65,14 @@ for step in "$@"; do
                 > "$GRAFT_REPO_ROOT/$OUT/copyprof.out" 2> "$GRAFT_REPO_ROOT/$OUT/copyprof.err")
             rc=$?; echo "=== copyprof rc=$rc" | tee -a "$OUT/steps.log"
             [ $rc -eq 0 ] || exit $rc ;;
+        copypmc)  # FETCH_SIZE / WRITE_SIZE of every copy_sweep variant (one launch round, 256 MiB)
+            for ctr in FETCH_SIZE WRITE_SIZE; do
+                (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv \
+                    -d "$GRAFT_REPO_ROOT/$OUT/copypmc_$ctr" -o copy -- "$GRAFT_REPO_ROOT/tools/copy_sweep" 256 1 2 \
+                    > "$GRAFT_REPO_ROOT/$OUT/copypmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$OUT/copypmc_$ctr.err")
+                rc=$?; echo "=== copypmc $ctr rc=$rc" | tee -a "$OUT/steps.log"
+                [ $rc -eq 0 ] || exit $rc
+            done ;;
         fanskew)
             run fanskew 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 skew ;;
         fanlayout)
