@@ -7,11 +7,15 @@ ABI (mi_reduce: inout += in over the whole bucket, inputs resident in HBM).
 
   python bench.py [--gpus N --steps K --warmup W] [--config c2|c3-bf16|c3-fp16|c4|...]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+With --gpus N > 1 and no launcher (WORLD_SIZE unset), bench.py starts the N
+rank processes itself and relays rank 0's line.
 
 Multi-GPU: the element range is sharded — every rank reduces
 its own 1 GiB bucket shard with no data-path collective ("scaling": "weak");
 torch.distributed is used only for the barrier and the max-over-ranks time.
-Rank 0 prints ONE JSON line.
+Rank 0 prints ONE JSON line.  After the timed region every rank re-fills its
+bucket, runs one more reduce and compares all of its elements bit for bit with
+a torch-computed fold (`parity` in the line; exit 3 on any mismatch).
 """
 from __future__ import annotations
 
@@ -170,6 +174,75 @@ def plan(n_total, es, rank, world, scaling):
     return hi.value - lo.value, lo.value, n_total * es
 
 
+def expected_result(ins, k, dt, op, flags):
+    """The whole bucket's expected result, computed on the device by plain
+    torch ops, independent of the kernels: the left fold acc = ins[0];
+    acc = op(ins[j], acc) of ccl_comp_reduce's CCL_REDUCE loop
+    (src/comp/comp.cpp:31-58), chained as the reference chains K-1 calls.
+    fp32 add is IEEE RNE on both sides, so the comparison is bit-exact; a
+    bf16/fp16 fold computes in fp32 and rounds once (RNE) per step, or once
+    at the end under F_ACC_FP32 (ccl_comp_batch_reduce keep-precision,
+    comp.cpp:214-234).  Integer prod wraps in two's complement, as in C++."""
+    import torch
+    lp = dt in (8, 11)
+    acc = ins[0].float() if lp else ins[0].clone()
+    for j in range(1, k):
+        x = ins[j].float() if lp else ins[j]
+        if op == 0:
+            acc = acc + x
+        elif op == 1:
+            acc = acc * x
+        elif op == 2:
+            acc = torch.minimum(x, acc)
+        else:
+            acc = torch.maximum(x, acc)
+        if lp and not (flags & 0x4):
+            acc = to_storage(acc, dt, flags).float()  # storage precision after every step
+    return to_storage(acc, dt, flags) if lp else acc
+
+
+def to_storage(acc, dt, flags):
+    """fp32 -> bf16/fp16 as the reference rounds: fp16 RNE (cvtps_ph, imm 0);
+    bf16 RNE under F_BF16_RNE (avx512bf VCVTNEPS2BF16), otherwise truncation
+    to the high 16 bits (scalar and avx512f impls, bf16.cpp:50-61)."""
+    import torch
+    if dt == 11 and not (flags & 0x2):
+        return (acc.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16)
+    return acc.to(torch.bfloat16 if dt == 11 else torch.float16)
+
+
+def shim_flags(dt):
+    """The semantic flags ccl_comp_reduce applies on this host (CPUID +
+    CCL_BF16 / CCL_FP16, comp.cpp's impl selection)."""
+    from oneccl_amd import comp
+    b, f = comp.impl_types()
+    return comp.bf16_flags(b) if dt == 11 else comp.fp16_flags(f) if dt == 8 else 0
+
+
+def count_mismatches(got, exp):
+    """Elements whose bits differ (NaN payloads included)."""
+    import torch
+    ib = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[got.element_size()]
+    return int(torch.ne(got.view(ib), exp.view(ib)).sum().item())
+
+
+def full_parity(run_once, ins, k, dt, op, flags, seed0, entry):
+    """Outside the timed region: re-fill the bucket, compute the expected
+    result on the device with torch, run ONE reduce through `run_once`, and
+    compare every element bit for bit.  Returns the JSON `parity` object."""
+    import torch
+    for j, t in enumerate(ins):
+        fill(t, seed0 + j)
+    exp = expected_result(ins, k, dt, op, flags)
+    torch.cuda.synchronize()
+    run_once()
+    torch.cuda.synchronize()
+    mism = count_mismatches(ins[0], exp)
+    del exp
+    return {"elements": ins[0].numel(), "mismatches": mism, "entry": entry,
+            "checker": "torch on the device (left fold in the reference's order, IEEE RNE; bits compared)"}
+
+
 def timed_steps(step, steps, warmup, stream, world, probe=10):
     """W untimed steps, then exactly K steps bracketed by a barrier and a
     device synchronize on both sides, issued back to back with one HIP event
@@ -259,8 +332,96 @@ def max_over_ranks(vals, world, device):
     return t.tolist()
 
 
+def sum_over_ranks(vals, world, device):
+    """Sum of each value over all ranks (parity counts)."""
+    if world <= 1:
+        return list(vals)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_plan(n, argv, port, base_env=None):
+    """(argv, env) of each of the n rank processes `bench.py --gpus n`
+    starts by itself when no launcher set WORLD_SIZE: the same script and
+    arguments, one rank per GPU, rendezvous on 127.0.0.1."""
+    env0 = dict(os.environ if base_env is None else base_env)
+    plans = []
+    for r in range(n):
+        env = dict(env0, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plans.append(([sys.executable, str(Path(__file__).resolve())] + list(argv), env))
+    return plans
+
+
+def launch_ranks(plans, timeout=None):
+    """Start every rank as a child process (never exec: the parent has made
+    no GPU call and makes none), relay rank 0's JSON line, and return the
+    exit code: 0 if every rank exited 0, else the first failing rank's code
+    (non-zero).  When one rank fails the others are stopped by PID, so a
+    rank left waiting in a barrier cannot hang the job."""
+    import subprocess
+    procs = []
+    for r, (argv, env) in enumerate(plans):
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      text=True))
+    out0 = []
+
+    def pump():
+        for line in procs[0].stdout:
+            out0.append(line)
+
+    import threading
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t_end = None if timeout is None else time.monotonic() + timeout
+    failed = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and not failed:
+            failed = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+        if all(c is not None for c in codes):
+            break
+        if t_end is not None and time.monotonic() > t_end:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            failed = failed or 124
+        time.sleep(0.05)
+    th.join(timeout=10)
+    for line in out0:
+        sys.stdout.write(line)
+    sys.stdout.flush()
+    if failed:
+        log(f"bench: a rank failed (exit {failed}); codes {[p.returncode for p in procs]}")
+    return failed if failed >= 0 else 128 - failed  # killed by signal s -> 128 + s
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` with no launcher: become the launcher.
+        # torch.cuda.device_count() does not initialise the GPU on this image.
+        import torch
+        argv = sys.argv[1:]
+        ndev = torch.cuda.device_count()
+        if args.dist_backend == "nccl" and ndev < args.gpus:
+            log(f"note: {args.gpus} ranks but {ndev} visible GPU(s): ranks share GPUs over a gloo process group")
+            argv += ["--dist-backend", "gloo"]
+        sys.exit(launch_ranks(rank_plan(args.gpus, argv, free_port())))
     import torch
     import torch.distributed as dist
 
@@ -304,16 +465,14 @@ def main():
             return m.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)  # inout += in
         return m.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
 
-    # quick correctness probe on one element before timing (c2 only)
-    if args.config == "c2":
-        a0, b0 = ins[1][123].item(), ins[0][123].item()
-        _lib.check(step(), "mi_reduce")
-        torch.cuda.synchronize()
-        expect = torch.tensor(a0, dtype=torch.float32) + torch.tensor(b0, dtype=torch.float32)
-        assert ins[0][123].item() == expect.item(), "probe mismatch"
-
     elapsed, avg_kern_ms, kern_ms = timed_steps(step, args.steps, args.warmup, stream, world)
     elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, coll_dev)
+
+    # the whole bucket checked bit for bit, outside the timed region (every
+    # rank checks its own; the line reports the sum over ranks)
+    seed0 = 0x5EED + 7919 * rank
+    parity = full_parity(lambda: _lib.check(step(), "mi_reduce"), ins, k, dt, op, flags, seed0,
+                         "mi_reduce" if k == 2 else "mi_reduce_multi")
 
     units_per_rank = n * es  # bucket bytes this rank reduced per step
     value = total_bytes * args.steps / elapsed / GiB
@@ -338,6 +497,22 @@ def main():
         dropin = {"value": round(n * es / GiB / statistics.median(tt), 2), "unit": "GiB/s",
                   "best": round(n * es / GiB / min(tt), 2), "calls": len(tt),
                   "entry": "ccl_comp_reduce (libccl_comp_hip.so, synchronous, oneCCL's C++ signature)"}
+        from oneccl_amd import comp as _comp
+        if dt == 8 and _comp.impl_types()[1] < 2:  # no fp16 impl: the reference computes nothing
+            dropin["parity"] = {"elements": 0, "mismatches": 0, "note": "fp16 impl computes nothing on this host"}
+        else:
+            dropin["parity"] = full_parity(
+                lambda: _lib.check_shim(shim.mi_ccl_comp_reduce(ins[1].data_ptr(), n, ins[0].data_ptr(), None, dt,
+                                                                op), "ccl_comp_reduce"),
+                ins, k, dt, op, shim_flags(dt), seed0 + 101, "ccl_comp_reduce")
+
+    # totals over ranks (each rank checked its own bucket shard)
+    parity["elements"], parity["mismatches"] = (int(x) for x in sum_over_ranks(
+        [parity["elements"], parity["mismatches"]], world, coll_dev))
+    if dropin:
+        dp = dropin["parity"]
+        dp["elements"], dp["mismatches"] = (int(x) for x in sum_over_ranks(
+            [dp["elements"], dp["mismatches"]], world, coll_dev))
 
     host_leg = None
     if rank == 0 and world == 1 and not args.no_host_leg and k == 2:
@@ -396,6 +571,7 @@ def main():
                                    "10 launches each between their own event pair, after the timed region",
                          "traffic_source": traffic.get("source") if traffic else None},
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         if strong:
             out["strong_split"] = strong
@@ -406,6 +582,10 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    bad = parity["mismatches"] + (dropin["parity"]["mismatches"] if dropin else 0)
+    if bad:
+        log(f"PARITY FAILURE: {bad} element(s) differ from the expected result")
+        sys.exit(3)
 
 
 def _host_pair(kind, nbytes):
@@ -518,30 +698,56 @@ def host_shard_probe(n, dt, es, op, flags):
                       "bucket_bytes": nn * es, "entry": "mi_reduce_multi_sync_sharded"}), flush=True)
 
 
-def pmc_traffic(config, algo_bytes):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass
-    (profiles/*pmc*.json, produced by tools/pmc_traffic.py), if present.  The
-    pass is a 1-GPU full-bucket run; a launch of another size (a strong-
-    scaling shard) gets the measured ratio to algorithmic bytes applied to
-    its own algorithmic bytes.  The newest round's pass wins."""
-    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+KERNEL_SOURCES = ("oneccl_amd/csrc/mi_reduce.hip", "oneccl_amd/csrc/reduce_kernels.hpp")
+
+
+def kernel_identity():
+    """sha256 (16 hex digits) of the kernel sources a PMC pass measured:
+    tools/pmc_traffic.py stores it with the pass, pmc_traffic() matches it."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        h.update((ROOT / rel).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def pmc_passes(config):
+    """Every committed PMC pass for `config` under profiles/ (any depth):
+    [(path, entry)] with the entry's recorded identity and time, if any."""
+    found = []
+    for p in (ROOT / "profiles").rglob("*pmc*.json"):
         try:
             d = json.loads(p.read_text())
         except (OSError, ValueError):
             continue
-        e = d.get(config)
-        if not isinstance(e, dict) or "hbm_bytes_per_launch" not in e:
-            continue
-        pmc_algo = e.get("algorithmic_bytes_per_launch")
-        if not pmc_algo:
-            continue
-        ratio = e["hbm_bytes_per_launch"] / pmc_algo
-        src = str(p.relative_to(ROOT))
-        if pmc_algo != algo_bytes:
-            src += f" (ratio {ratio:.6f} of a {pmc_algo}-B launch, applied to this {algo_bytes}-B launch)"
-        return {"bytes_per_launch": int(round(ratio * algo_bytes)), "ratio": round(ratio, 6), "source": src}
-    return None
+        e = d.get(config) if isinstance(d, dict) else None
+        if isinstance(e, dict) and "hbm_bytes_per_launch" in e and e.get("algorithmic_bytes_per_launch"):
+            found.append((p, e))
+    return found
 
+
+def pmc_traffic(config, algo_bytes):
+    """HBM bytes per launch from a committed rocprofv3 PMC pass (produced by
+    tools/pmc_traffic.py).  The pass chosen is the one recorded against the
+    kernel sources of this tree (kernel_identity); failing that, the most
+    recently recorded one, marked stale.  The pass is a 1-GPU full-bucket
+    run; a launch of another size (a strong-scaling shard) gets the measured
+    ratio to algorithmic bytes applied to its own algorithmic bytes."""
+    passes = pmc_passes(config)
+    if not passes:
+        return None
+    ident = kernel_identity()
+    current = [pe for pe in passes if pe[1].get("kernel_sources") == ident]
+    pool = current or passes
+    p, e = max(pool, key=lambda pe: (pe[1].get("recorded_utc", ""), str(pe[0])))
+    pmc_algo = e["algorithmic_bytes_per_launch"]
+    ratio = e["hbm_bytes_per_launch"] / pmc_algo
+    src = str(p.relative_to(ROOT))
+    src += " (kernel sources match this tree)" if current else " (STALE: recorded against other kernel sources)"
+    if pmc_algo != algo_bytes:
+        src += f" (ratio {ratio:.6f} of a {pmc_algo}-B launch, applied to this {algo_bytes}-B launch)"
+    return {"bytes_per_launch": int(round(ratio * algo_bytes)), "ratio": round(ratio, 6), "source": src,
+            "current": bool(current)}
 
 if __name__ == "__main__":
     if len(sys.argv) == 7 and sys.argv[1] == "--host-shard-probe":

@@ -91,6 +91,17 @@ int mi_ccl_comp_host_workers(void);
  * (elements/s; < 0 before it was timed) and how many buckets it will still
  * run on the GPU alone (after a split lost to it, or as a probe).  Diagnostic. */
 double mi_ccl_comp_split_gpu_rate(int pinned, unsigned* gpu_left);
+/* Test hooks for the adaptive split's bookkeeping (no reduce is run):
+ * take_gpu_alone = the decision an adapting thread makes before a bucket of
+ * that kind (1 = the GPU alone, consuming one scheduled GPU-alone bucket;
+ * 0 = split); split_feed = the update after a bucket of `count` elements,
+ * a split with a CPU head of `head` elements (t_head, t_tail seconds from
+ * its start) or, head = 0, a GPU-alone bucket of t_tail seconds.  The same
+ * functions the synchronous and asynchronous paths call.                   */
+int mi_ccl_comp_split_take_gpu_alone(int pinned);
+int mi_ccl_comp_split_feed(int pinned, size_t count, size_t head, double t_head, double t_tail);
+/* The dispatcher's thresholds and default shares in force (after env).     */
+int mi_ccl_comp_host_max(size_t* pageable, size_t* pinned, double* share, double* share_pinned);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

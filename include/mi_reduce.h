@@ -95,6 +95,8 @@ enum mi_dtype {
 #define MI_E_UNSUPPORTED (-2)  /* combination not implemented            */
 #define MI_E_NO_DEVICE (-3)    /* no HIP device visible                   */
 #define MI_E_RESOURCE (-4)     /* host resources (thread, memory) failed  */
+#define MI_E_EXITING (-5)      /* process exit began before an asynchronous
+                                  request ran; it was not run              */
 
 #define MI_MAX_INPUTS 16 /* the reference's monolithic fan-in covers 16 ranks
                             (src/kernels/kernels.cl:268)                   */
@@ -176,6 +178,17 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count,
                     int dtype, int op, unsigned flags, int device,
                     mi_request_t* req);
 int mi_test(mi_request_t req, int* done);
+/* mi_reduce_start that also times the request where it runs: a staged
+ * request on the staging worker's clock (from when it starts, after the
+ * thread's earlier work), a direct one by a HIP event pair around its
+ * launch.  mi_request_run_time gives that duration in seconds once the
+ * request is done (MI_E_INVALID before, or for an untimed direct request).
+ * The drop-in's adaptive dispatcher times its GPU-alone buckets with it, so
+ * the rate it learns excludes the delay before the caller polls.          */
+int mi_reduce_start_timed(const void* const* inputs, int k, void* out, size_t count,
+                          int dtype, int op, unsigned flags, int device,
+                          mi_request_t* req);
+int mi_request_run_time(mi_request_t req, double* seconds);
 /* The cooperative split as a request: elements [0, head_count) are folded by
  * `head_fold` (a host reduce with mi_host_reduce's signature and semantics,
  * include/mi_host_reduce.h) on the calling thread's staging worker while the
@@ -316,6 +329,11 @@ int mi_get_launch_config(int* block, int* unroll, int* max_blocks);
 /* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS).  Under a
  * cap the reduce, copy and conversion kernels stride over the buffer.     */
 int mi_set_max_blocks(int max_blocks);
+/* CPUs the library's helper threads (staging worker, drain thread) run on:
+ * the process's allowed set read at load (/proc/self/status), so helpers of
+ * a worker oneCCL pinned to one core do not share that core.  0 = helpers
+ * inherit their creator's mask (MI_REDUCE_HELPER_AFFINITY=inherit).       */
+int mi_helper_cpu_count(void);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,9 @@ MI_API = [
     ("mi_convert_sync", c_int, [c_void_p, c_int, c_void_p, c_int, c_size_t, c_uint, c_int]),
     ("mi_reduce_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
                                 POINTER(c_void_p)]),
+    ("mi_reduce_start_timed", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
+                                      POINTER(c_void_p)]),
+    ("mi_request_run_time", c_int, [c_void_p, POINTER(c_double)]),
     ("mi_reduce_split_start", c_int, [POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_int, c_uint, c_int,
                                       c_size_t, c_void_p, POINTER(c_void_p)]),
     ("mi_request_split_times", c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
@@ -74,6 +77,7 @@ MI_API = [
     ("mi_set_host_mode", c_int, [c_int]),
     ("mi_set_sync_mode", c_int, [c_int]),
     ("mi_set_unaligned_vectors", c_int, [c_int]),
+    ("mi_helper_cpu_count", c_int, []),
 ]
 
 # mirrors include/mi_ccl_comp.h
@@ -104,6 +108,9 @@ SHIM_API = [
     ("mi_ccl_comp_split_share", c_double, [c_int]),
     ("mi_ccl_comp_host_workers", c_int, []),
     ("mi_ccl_comp_split_gpu_rate", c_double, [c_int, POINTER(c_uint)]),
+    ("mi_ccl_comp_split_take_gpu_alone", c_int, [c_int]),
+    ("mi_ccl_comp_split_feed", c_int, [c_int, c_size_t, c_size_t, c_double, c_double]),
+    ("mi_ccl_comp_host_max", c_int, [POINTER(c_size_t), POINTER(c_size_t), POINTER(c_double), POINTER(c_double)]),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

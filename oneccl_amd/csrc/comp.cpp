@@ -146,6 +146,7 @@ static HostMax parse_host_max() {
     m.share = std::min(0.95, std::max(0.0, sh ? atof(sh) : kHostShareDefault));
     m.share_pinned = std::min(0.95, std::max(0.0, shp ? atof(shp) : kHostSharePinnedDefault));
     if (m.pageable == 0) m.share = m.share_pinned = 0;  // "always the GPU"
+    if (m.pinned == 0) m.share_pinned = 0;               // pinned buckets: always the GPU, never split
     const char* ad = getenv("CCL_COMP_HOST_SHARE_ADAPT");
     const bool adapt = !(ad && atoi(ad) == 0);
     m.adapt = adapt && !sh && m.share > 0;
@@ -512,6 +513,29 @@ static void gpu_alone_timed(int pk, size_t count, double t) {
     g = g < 0 ? r : 0.5 * g + 0.5 * r;
 }
 
+// An adapting thread's next bucket of kind pk: the GPU alone (timed) while
+// split_verdict has GPU-alone buckets scheduled; consumes one.
+static bool take_gpu_alone(int pk) {
+    if (t_split.gpu_left[pk] == 0) return false;
+    t_split.gpu_left[pk]--;
+    return true;
+}
+
+// After a split of `count` elements whose head of `head` took t_cpu seconds
+// on the CPU and whose tail took t_gpu on the GPU (both from the split's
+// start): move the share halfway toward the balance point, kept within
+// [0.1, 0.9], and judge the split against the GPU alone.  A thread's first
+// split of a kind only warms up.  Shared by the synchronous (coop_fold) and
+// asynchronous (settle_split) paths.
+static void split_update(int pk, size_t count, size_t head, double t_cpu, double t_gpu) {
+    if (t_cpu <= 0 || t_gpu <= 0 || head == 0 || head >= count) return;
+    if (t_split.calls[pk]++ == 0) return;
+    const double r_cpu = (double)head / t_cpu, r_gpu = (double)(count - head) / t_gpu;
+    double& cur = t_split.share[pk];
+    cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
+    split_verdict(pk, count, std::max(t_cpu, t_gpu));
+}
+
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -520,12 +544,10 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
               int pinned, bool adapt) {
     const int pk = pinned ? 1 : 0;
     double& cur = t_split.share[pk];
-    unsigned& calls = t_split.calls[pk];
     if (adapt) {
         if (cur < 0) cur = share;
         share = cur;
-        if (t_split.gpu_left[pk] > 0) {  // the GPU alone, timed
-            t_split.gpu_left[pk]--;
+        if (take_gpu_alone(pk)) {  // the GPU alone, timed
             const double t0 = now_s();
             const int rc = mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
             if (rc == 0) gpu_alone_timed(pk, count, now_s() - t0);
@@ -559,11 +581,7 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     const int wrc = mi_wait(r);
     if (t_gpu < 0) t_gpu = now_s() - t0;
     (void)mi_request_free(r);
-    if (adapt && calls++ > 0 && hrc == 0 && wrc == 0 && t_cpu > 0 && t_gpu > 0) {
-        const double r_cpu = (double)s / t_cpu, r_gpu = (double)(count - s) / t_gpu;
-        cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
-        split_verdict(pk, count, std::max(t_cpu, t_gpu));
-    }
+    if (adapt && hrc == 0 && wrc == 0) split_update(pk, count, s, t_cpu, t_gpu);
     return wrc ? wrc : hrc;
 }
 
@@ -654,27 +672,25 @@ struct SplitIssued {      // an adaptive split issued by start_fold, for the sha
     mi_request_t req = nullptr;
     int kind = 0;            // 0: some operand pageable, 1: all pinned
     size_t count = 0, head = 0;  // head 0: a timed GPU-alone bucket
-    double t_start = 0;      // GPU-alone buckets: when it was issued
     bool settled = false;    // the share update is done (or not wanted)
 };
 
-// On the caller's thread, once its split request is done: move the thread's
-// share for that pointer kind halfway toward the balance point, as coop_fold
-// does; a thread's first split of a kind only warms up.
+// On the caller's thread, once its split request is done: the share update
+// coop_fold makes, from times measured where the request ran (the staging
+// worker's clock, or a HIP event pair around the zero-copy kernel), never
+// from when the caller happened to poll it: a oneCCL worker polls between
+// other entries, and that delay would read as a slow GPU.
 void settle_split(SplitIssued& sp) {
     if (!sp.req || sp.settled) return;
     sp.settled = true;
-    if (sp.head == 0) {  // a GPU-alone bucket: its time as the caller saw it complete
-        gpu_alone_timed(sp.kind, sp.count, now_s() - sp.t_start);
+    if (sp.head == 0) {  // a GPU-alone bucket
+        double t = 0;
+        if (mi_request_run_time(sp.req, &t) == 0) gpu_alone_timed(sp.kind, sp.count, t);
         return;
     }
     double th = 0, tt = 0;
-    if (mi_request_split_times(sp.req, &th, &tt) != 0 || th <= 0 || tt <= 0) return;
-    if (t_split.calls[sp.kind]++ == 0) return;
-    const double r_cpu = (double)sp.head / th, r_gpu = (double)(sp.count - sp.head) / tt;
-    double& cur = t_split.share[sp.kind];
-    cur = std::min(0.9, std::max(0.1, 0.5 * cur + 0.5 * r_cpu / (r_cpu + r_gpu)));
-    split_verdict(sp.kind, sp.count, std::max(th, tt));
+    if (mi_request_split_times(sp.req, &th, &tt) != 0) return;
+    split_update(sp.kind, sp.count, sp.head, th, tt);
 }
 
 int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags,
@@ -690,16 +706,13 @@ int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, i
             share = t_split.share[pk];
         }
         const int limit = pk ? m.split_workers_pinned : m.split_workers;
-        if (adapt && t_split.gpu_left[pk] > 0 && sp && !sp->req) {  // the GPU alone, timed to completion
-            t_split.gpu_left[pk]--;
-            const double t0 = now_s();
-            const int rc = mi_reduce_start(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
+        if (adapt && sp && !sp->req && take_gpu_alone(pk)) {  // the GPU alone, timed where it runs
+            const int rc = mi_reduce_start_timed(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
             if (rc == 0) {
                 sp->req = *r;
                 sp->kind = pk;
                 sp->count = count;
                 sp->head = 0;
-                sp->t_start = t0;
             }
             return rc;
         }
@@ -1235,6 +1248,31 @@ int mi_ccl_env_reload(void) {
 }
 
 double mi_ccl_comp_split_share(int pinned) { return t_split.share[pinned ? 1 : 0]; }
+
+int mi_ccl_comp_split_take_gpu_alone(int pinned) { return take_gpu_alone(pinned ? 1 : 0) ? 1 : 0; }
+
+int mi_ccl_comp_split_feed(int pinned, size_t count, size_t head, double t_head, double t_tail) {
+    MI_SHIM_GUARD({
+        const int pk = pinned ? 1 : 0;
+        const HostMax m = mi_host_max();
+        double& cur = t_split.share[pk];
+        if (cur < 0) cur = pk ? m.share_pinned : m.share;  // as coop_fold starts a thread's share
+        if (head == 0) gpu_alone_timed(pk, count, t_tail);
+        else split_update(pk, count, head, t_head, t_tail);
+        return 0;
+    });
+}
+
+int mi_ccl_comp_host_max(size_t* pageable, size_t* pinned, double* share, double* share_pinned) {
+    MI_SHIM_GUARD({
+        const HostMax m = mi_host_max();
+        if (pageable) *pageable = m.pageable;
+        if (pinned) *pinned = m.pinned;
+        if (share) *share = m.share;
+        if (share_pinned) *share_pinned = m.share_pinned;
+        return 0;
+    });
+}
 
 int mi_ccl_comp_host_workers(void) { return host_workers(); }
 

@@ -549,9 +549,32 @@ struct DevCtx {
 // the cooperative split's CPU head: measured with pinned workers, the GPU
 // path then ran at half its rate and the split below one core
 // (profiles/round2_dispatch/workers_pinned_inherit.jsonl).  Helpers therefore
-// take the CPU set the library was loaded with (the process's, before any
-// worker pinned itself); MI_REDUCE_HELPER_AFFINITY=inherit keeps the
-// creator's.
+// take the process's CPU set: the main thread's allowed list
+// (/proc/self/status describes the thread-group leader, which oneCCL does
+// not pin), read at library load -- not the loading thread's own mask, which
+// is one core when the library is dlopen'ed lazily from a pinned worker.
+// MI_REDUCE_HELPER_AFFINITY=inherit keeps the creator's; mi_helper_cpu_count()
+// reports the set chosen.
+bool parse_cpu_list(const char* s, cpu_set_t* out) {
+    CPU_ZERO(out);
+    while (*s && *s != '\n') {
+        char* end = nullptr;
+        const long a = strtol(s, &end, 10);
+        if (end == s || a < 0) return false;
+        long b = a;
+        s = end;
+        if (*s == '-') {
+            b = strtol(s + 1, &end, 10);
+            if (end == s + 1 || b < a) return false;
+            s = end;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++) CPU_SET((int)c, out);
+        if (*s == ',') s++;
+        else if (*s && *s != '\n') return false;
+    }
+    return CPU_COUNT(out) > 0;
+}
+
 struct HelperCpus {
     cpu_set_t mask;
     bool use = false;
@@ -559,7 +582,18 @@ struct HelperCpus {
         CPU_ZERO(&mask);
         const char* e = getenv("MI_REDUCE_HELPER_AFFINITY");
         if (e && strcmp(e, "inherit") == 0) return;
-        use = sched_getaffinity(0, sizeof(mask), &mask) == 0 && CPU_COUNT(&mask) > 0;
+        if (FILE* f = fopen("/proc/self/status", "r")) {
+            char line[4096];
+            while (fgets(line, sizeof line, f))
+                if (strncmp(line, "Cpus_allowed_list:", 18) == 0) {
+                    const char* p = line + 18;
+                    while (*p == ' ' || *p == '\t') p++;
+                    use = parse_cpu_list(p, &mask);
+                    break;
+                }
+            fclose(f);
+        }
+        if (!use) use = sched_getaffinity(0, sizeof(mask), &mask) == 0 && CPU_COUNT(&mask) > 0;
     }
 };
 const HelperCpus g_helper_cpus;  // at library load
@@ -643,32 +677,55 @@ struct Drain {
     ~Drain() { (void)finish(); }
 };
 
-// Process exit against threads that are still exiting.  A thread's contexts
-// are freed by its thread_local destructors (hipFree of the staging buffers
-// synchronises the device and takes milliseconds).  A host program may exit
-// while such a thread is still in them: Python's Thread.join(), for one,
-// returns before the OS thread has run its thread_local destructors.  The
-// HIP runtime's own exit-time teardown then pulls the device from under
-// those calls (a SIGSEGV inside libamdhip64 from __call_tls_dtors).  So an
-// exit handler, registered after the runtime's (at the first context, when
-// HIP is initialised, so it runs before them), marks the process as exiting
-// and waits up to 2 s for teardowns already in HIP calls; later ones leave
-// their contexts to the process's end.
+// Process exit against threads that are still exiting or still working.  A
+// thread's contexts are freed by its thread_local destructors (hipFree of
+// the staging buffers synchronises the device and takes milliseconds), and
+// its staging worker (t_stage) finishes the thread's un-waited asynchronous
+// requests when the thread exits.  A host program may exit while either is
+// still going: Python's Thread.join(), for one, returns before the OS thread
+// has run its thread_local destructors.  The HIP runtime's own exit-time
+// teardown then pulls the device from under those calls (a SIGSEGV inside
+// libamdhip64 from __call_tls_dtors, profiles/round2_dispatch/
+// exit_crash_trace.txt).
+//
+// So every such section -- a context teardown, and every job a staging
+// worker runs -- holds an ExitGuard while it makes HIP calls.  An exit
+// handler, registered after the runtime's (at the first context, when HIP is
+// initialised, so it runs before the runtime's), marks the process as
+// exiting and then waits, with no time limit, until no guard is held.  A
+// section that would start after that mark makes no HIP call: a teardown
+// leaves its context to the process's end, a job fails with MI_E_EXITING.
+// The counter is raised before the mark is read (both sequentially
+// consistent), so either the section sees the mark or the handler sees the
+// section.
 std::atomic<bool> g_exiting{false};
-std::atomic<int> g_teardowns{0};
+std::atomic<int> g_active{0};
 
 void at_process_exit() {
     g_exiting.store(true);
-    for (int i = 0; i < 2000 && g_teardowns.load() > 0; i++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    while (g_active.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
 }
+
+struct ExitGuard {
+    bool entered;
+    ExitGuard() {
+        g_active.fetch_add(1);
+        entered = !g_exiting.load();
+        if (!entered) g_active.fetch_sub(1);
+    }
+    ~ExitGuard() {
+        if (entered) g_active.fetch_sub(1);
+    }
+    ExitGuard(const ExitGuard&) = delete;
+    ExitGuard& operator=(const ExitGuard&) = delete;
+};
 
 struct ThreadCtx {
     std::vector<DevCtx*> devs;
     ~ThreadCtx() {
-        g_teardowns.fetch_add(1);
-        if (!g_exiting.load())
+        ExitGuard g;
+        if (g.entered)
             for (DevCtx* d : devs) delete d;
-        g_teardowns.fetch_sub(1);
     }
 };
 thread_local ThreadCtx t_ctx;
@@ -744,7 +801,7 @@ struct HostCopy {
 
 int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
                  unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr,
-                 HostCopy* post = nullptr) {
+                 HostCopy* post = nullptr, hipEvent_t* t_start = nullptr) {
     *ctx = nullptr;
     *used = 0;
     const size_t es = dtype_size(dt);
@@ -805,6 +862,10 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     if (!all_dev && direct && host_mode() == MI_HOST_STAGED) direct = false;
     if (all_dev || direct) {
         *used = 1;
+        if (t_start) {  // a timed request: an event pair around the one launch
+            MI_HIP(hipEventCreateWithFlags(t_start, hipEventDefault));
+            MI_HIP(hipEventRecord(*t_start, d->stream[0]));
+        }
         return launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
     }
 
@@ -953,6 +1014,7 @@ struct AsyncJob {
     size_t head = 0;
     mi_host_fold_t head_fold = nullptr;
     double t_head = -1.0, t_tail = -1.0;  // seconds from the split's start (run_split)
+    double t_run = -1.0;                  // seconds the worker spent running it (after `prior`)
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
@@ -971,6 +1033,10 @@ struct AsyncJob {
 
 int run_split(AsyncJob& j);
 int split_job(AsyncJob& j) { return run_split(j); }
+
+double mono_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct StageWorker {
     std::thread th;
@@ -1019,14 +1085,27 @@ struct StageWorker {
                 q.pop_front();
             }
             int rc = 0;
-            for (hipEvent_t e : j->prior) {
-                const hipError_t he = hipEventSynchronize(e);
-                if (he != hipSuccess && !rc) rc = hip_fail(he, "waiting for earlier work of the submitting thread");
-                (void)hipEventDestroy(e);
+            {
+                ExitGuard g;  // the exit handler waits for a job that has started
+                if (!g.entered) {
+                    rc = fail(MI_E_EXITING, "the process is exiting: asynchronous request not run");
+                    j->prior.clear();  // their events go with the process
+                } else {
+                    for (hipEvent_t e : j->prior) {
+                        const hipError_t he = hipEventSynchronize(e);
+                        if (he != hipSuccess && !rc)
+                            rc = hip_fail(he, "waiting for earlier work of the submitting thread");
+                        (void)hipEventDestroy(e);
+                    }
+                    j->prior.clear();
+                    const double t0 = mono_s();
+                    if (!rc)
+                        rc = j->head_fold ? split_job(*j)
+                                          : reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags,
+                                                        j->device);
+                    j->t_run = mono_s() - t0;  // published by the done flag below
+                }
             }
-            j->prior.clear();
-            if (!rc) rc = j->head_fold ? split_job(*j) : reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op,
-                                                                       j->flags, j->device);
             {
                 std::lock_guard<std::mutex> lk(j->mu);
                 j->rc = rc;
@@ -1040,7 +1119,9 @@ struct StageWorker {
         }
     }
     // Thread exit: finish every submitted job (they write the callers'
-    // buffers), then stop.
+    // buffers), then stop.  Each job holds an ExitGuard, so a process exit
+    // that overlaps this join waits for the job in progress, and the jobs
+    // after it fail at once without touching HIP (see at_process_exit).
     ~StageWorker() {
         if (!th.joinable()) return;
         {
@@ -1063,9 +1144,6 @@ thread_local bool t_async_issued = false;
 // keep-precision truncated tail), polling the GPU part between them: both
 // parts' durations are known even when the GPU finishes first, and the
 // caller adapts its share from them (mi_request_split_times).
-double mono_s() {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 int run_split(AsyncJob& j) {
     const size_t es = dtype_size(j.dt);
@@ -1330,11 +1408,13 @@ struct mi_request {
     hipEvent_t ev[2] = {nullptr, nullptr};
     int nev = 0;
     int device = -1;
+    hipEvent_t t0 = nullptr;        // timed direct request: recorded before its launch (ev[0] ends it)
     std::shared_ptr<AsyncJob> job;  // staged work running on the calling thread's worker
 };
 
-int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
-                    unsigned flags, int device, mi_request_t* req) {
+namespace {
+int reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op, unsigned flags,
+                 int device, mi_request_t* req, bool timed) {
     return guarded([&]() -> int {
         if (!req) return fail(MI_E_INVALID, "null request pointer");
         *req = nullptr;
@@ -1372,9 +1452,15 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
         }
         DevCtx* d = nullptr;
         int used = 0;
-        int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used);
-        if (rc) return rc;
+        hipEvent_t t0 = nullptr;
+        int rc = reduce_issue(inputs, k, out, count, dtype, op, flags, device, &d, &used, nullptr, nullptr,
+                              timed ? &t0 : nullptr);
+        if (rc) {
+            if (t0) (void)hipEventDestroy(t0);
+            return rc;
+        }
         mi_request* r = new mi_request();
+        r->t0 = t0;
         if (d) {
             r->device = d->device;
             int prev = 0;
@@ -1382,7 +1468,7 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
             if (prev != d->device) MI_HIP(hipSetDevice(d->device));
             for (int s = 0; s < 2 && rc == 0; s++) {
                 if (!(used & (1 << s))) continue;
-                hipError_t e = hipEventCreateWithFlags(&r->ev[r->nev], hipEventDisableTiming);
+                hipError_t e = hipEventCreateWithFlags(&r->ev[r->nev], t0 ? hipEventDefault : hipEventDisableTiming);
                 if (e == hipSuccess) e = hipEventRecord(r->ev[r->nev], d->stream[s]);
                 if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
                 r->nev++;
@@ -1396,6 +1482,37 @@ int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, i
         *req = r;
         return 0;
     });
+}
+}  // namespace
+
+int mi_reduce_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                    unsigned flags, int device, mi_request_t* req) {
+    return reduce_start(inputs, k, out, count, dtype, op, flags, device, req, false);
+}
+
+int mi_reduce_start_timed(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
+                          unsigned flags, int device, mi_request_t* req) {
+    return reduce_start(inputs, k, out, count, dtype, op, flags, device, req, true);
+}
+
+int mi_request_run_time(mi_request_t req, double* seconds) {
+    if (!req || !seconds) return fail(MI_E_INVALID, "null argument");
+    if (req->job) {
+        std::lock_guard<std::mutex> lk(req->job->mu);
+        if (!req->job->done || req->job->rc || req->job->t_run < 0) return fail(MI_E_INVALID, "request not finished");
+        *seconds = req->job->t_run;
+        return 0;
+    }
+    if (!req->t0 || req->nev != 1) return fail(MI_E_INVALID, "not a timed request");
+    float ms = 0;
+    const hipError_t e = hipEventElapsedTime(&ms, req->t0, req->ev[0]);
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return fail(MI_E_INVALID, "request not finished");
+    }
+    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+    *seconds = ms * 1e-3;
+    return 0;
 }
 
 int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t count, int dtype, int op,
@@ -1482,6 +1599,7 @@ int mi_request_free(mi_request_t req) {
     if (req->job) (void)req->job->wait();  // the job writes the caller's buffers: never leave it running
     for (int i = 0; i < req->nev; i++)
         if (req->ev[i]) (void)hipEventDestroy(req->ev[i]);
+    if (req->t0) (void)hipEventDestroy(req->t0);
     delete req;
     return 0;
 }
@@ -1705,6 +1823,8 @@ size_t mi_dtype_size(int dtype) { return dtype_size(dtype); }
 const char* mi_last_error(void) { return g_last_error.c_str(); }
 
 int mi_version(void) { return 100; }  // 0.1.0
+
+int mi_helper_cpu_count(void) { return g_helper_cpus.use ? CPU_COUNT(&g_helper_cpus.mask) : 0; }
 
 int mi_device_count(void) {
     int n = 0;

@@ -1,0 +1,159 @@
+"""bench.py as its own launcher (CPU): `python bench.py --gpus N` with no
+WORLD_SIZE starts N rank processes, relays rank 0's JSON line, and exits
+non-zero when any rank fails.  Also the full-bucket parity checker's
+expected-result fold and the helper-thread CPU set (no GPU needed)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import textwrap
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+
+def test_rank_plan_env():
+    plans = bench.rank_plan(4, ["--gpus", "4", "--steps", "3"], 29555, base_env={"KEEP": "1"})
+    assert len(plans) == 4
+    for r, (argv, env) in enumerate(plans):
+        assert argv[0] == sys.executable and argv[1].endswith("bench.py")
+        assert argv[2:] == ["--gpus", "4", "--steps", "3"]
+        assert env["RANK"] == env["LOCAL_RANK"] == str(r)
+        assert env["WORLD_SIZE"] == env["LOCAL_WORLD_SIZE"] == "4"
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29555"
+        assert env["KEEP"] == "1"
+
+
+def _fake(code: str):
+    """A fake rank: python -c <code> with the planned env."""
+    return [sys.executable, "-c", textwrap.dedent(code)]
+
+
+def test_launch_relays_rank0_line(capfd):
+    code = """
+    import json, os
+    r = int(os.environ["RANK"])
+    if r == 0:
+        print(json.dumps({"metric": "m", "n_gpus": int(os.environ["WORLD_SIZE"])}), flush=True)
+    """
+    plans = [(_fake(code), env) for _, env in bench.rank_plan(3, [], 1, base_env={})]
+    rc = bench.launch_ranks(plans, timeout=60)
+    out = capfd.readouterr().out.strip().splitlines()
+    assert rc == 0
+    assert json.loads(out[-1]) == {"metric": "m", "n_gpus": 3}
+
+
+def test_launch_fails_when_a_rank_fails_and_stops_the_rest(capfd):
+    code = """
+    import os, sys, time
+    r = int(os.environ["RANK"])
+    if r == 1:
+        sys.exit(7)
+    time.sleep(60)          # a rank left waiting (e.g. in a barrier)
+    """
+    plans = [(_fake(code), env) for _, env in bench.rank_plan(3, [], 1, base_env={})]
+    import time
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(plans, timeout=120)
+    assert rc == 7
+    assert time.monotonic() - t0 < 30  # the waiting ranks were stopped, not waited for
+
+
+def test_launch_times_out():
+    plans = [(_fake("import time; time.sleep(60)"), env) for _, env in bench.rank_plan(2, [], 1, base_env={})]
+    assert bench.launch_ranks(plans, timeout=1) != 0
+
+
+def test_launch_killed_rank_maps_to_128_plus_signal():
+    code = """
+    import os, signal
+    if os.environ["RANK"] == "1":
+        os.kill(os.getpid(), signal.SIGKILL)
+    """
+    plans = [(_fake(code), env) for _, env in bench.rank_plan(2, [], 1, base_env={})]
+    assert bench.launch_ranks(plans, timeout=60) == 128 + 9
+
+
+def test_bench_gpus2_without_launcher_runs_two_ranks_on_cpu_box():
+    """The real script: --gpus 2 with no WORLD_SIZE re-launches itself as two
+    ranks.  Without a GPU each rank fails at its first device call, so the
+    job must exit non-zero (and not report a 1-rank line)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--no-host-leg"], capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode == 0:  # a GPU box: a 2-rank line
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        assert line["n_gpus"] == 2
+    else:
+        assert "metric" not in r.stdout
+        assert "ranks share GPUs" in r.stderr or "a rank failed" in r.stderr
+
+
+def test_expected_result_fold_matches_oracle():
+    """The bench's on-device checker (torch ops) folds in the reference's
+    order and rounds like it: checked here on CPU tensors against the oracle
+    (the restatement of src/comp), for every config the bench runs."""
+    import numpy as np
+    import torch
+
+    import oracle
+    rng = np.random.default_rng(3)
+    n = 4099
+    for name, (desc, dt, es, op, k, bucket, flags) in bench.CONFIGS.items():
+        if dt == 9:
+            ins = [rng.standard_normal(n).astype(np.float32) for _ in range(k)]
+        elif dt in (4, 6):
+            ins = [rng.integers(-1000, 1000, n).astype(oracle.NP_DTYPE[dt]) for _ in range(k)]
+        else:
+            f = [rng.standard_normal(n).astype(np.float32) for _ in range(k)]
+            ins = [oracle.f32_to_bf16(x, True) if dt == 11 else oracle.f32_to_fp16(x) for x in f]
+        tdt = bench.torch_dtype(dt)
+        view = {2: torch.int16, 4: torch.int32, 8: torch.int64}[es]
+        tins = [torch.from_numpy(x.copy()).view(view).view(tdt) if dt in (8, 11) else torch.from_numpy(x.copy())
+                for x in ins]
+        got = bench.expected_result(tins, k, dt, op, flags)
+        if flags & 0x4:  # keep-precision: fp32 accumulate, one rounding (ccl_comp_batch_reduce)
+            exp = oracle.lp_fanin_acc_fp32(ins, dt, op, bool(flags & 0x2), bool(flags & 0x1))
+        else:
+            exp = oracle.fanin(ins, dt, op, oracle.BF16_AVX512BF if flags & 0x2 else oracle.BF16_SCALAR,
+                               oracle.FP16_AVX512F)
+        gb = got.view(view).numpy()
+        assert gb.tobytes() == exp.view(gb.dtype).tobytes(), name
+
+
+def test_bf16_truncation_in_checker():
+    """Without F_BF16_RNE (scalar / avx512f impls) the checker truncates."""
+    import torch
+    acc = torch.tensor([1.0 + 2 ** -8 + 2 ** -10], dtype=torch.float32)  # RNE rounds up, truncation down
+    t = bench.to_storage(acc, 11, 0).view(torch.int16).item() & 0xFFFF
+    r = bench.to_storage(acc, 11, 0x2).view(torch.int16).item() & 0xFFFF
+    assert t == 0x3F80 and r == 0x3F81
+
+
+def test_helper_threads_take_the_process_cpu_set():
+    """libmi_reduce.so loaded from a thread pinned to one core still gives
+    its helper threads the process's CPU set."""
+    if len(os.sched_getaffinity(0)) < 2:
+        pytest.skip("needs 2+ CPUs")
+    code = textwrap.dedent("""
+        import os, sys, threading
+        sys.path.insert(0, sys.argv[1])
+        res = {}
+        def loader():
+            os.sched_setaffinity(0, {min(os.sched_getaffinity(0))})
+            from oneccl_amd import _lib
+            res["n"] = _lib.mi().mi_helper_cpu_count()
+        t = threading.Thread(target=loader); t.start(); t.join()
+        print(res["n"], len(os.sched_getaffinity(0)))
+    """)
+    r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, total = (int(x) for x in r.stdout.split())
+    assert n == total > 1

@@ -113,6 +113,10 @@ for step in "$@"; do
                 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo &&
             run dist2_strong 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29534 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --scaling strong ;;
+        dist2self)  # bench.py as its own launcher: --gpus 2 with no WORLD_SIZE (both ranks share the box's GPU)
+            run dist2self 300 python bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --no-cpu-baseline ;;
+        pmcjson)  # the PMC passes of `pmc` summarised into profiles-ready JSON
+            python tools/pmc_traffic.py "$OUT/pmc.json" "c2=$OUT:3221225472" > "$OUT/pmcjson.out" 2>&1 ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
         sizes_fp32)
