@@ -24,13 +24,16 @@ namespace mi_host {
 
 typedef void (*FoldFn)(const void* const*, int, void*, size_t, unsigned);
 
-template <typename V, int OP, bool INOUT_FIRST>
+template <typename V, int OP, bool INOUT_FIRST, bool ACC32>
 inline typename V::F vop(typename V::F x, typename V::F a) {  // acc' = op(in = x, acc = a)
     switch (OP) {
         // ADDPS / MULPS(in, acc): the compiler may swap the operands of the
-        // commutative intrinsics, so the both-NaN choice is made explicit
-        case MI_OP_SUM: return V::nan_first(V::add(x, a), x, a);
-        case MI_OP_PROD: return V::nan_first(V::mul(x, a), x, a);
+        // commutative intrinsics, so the both-NaN choice is made explicit.
+        // The fp32 accumulation of keep-precision is CCL_REDUCE(float)'s
+        // `acc += tmp` (comp.cpp:223-229), whose accumulator NaN wins
+        // (tests/golden/ref_comp_vectors.npz).
+        case MI_OP_SUM: return ACC32 ? V::nan_first(V::add(x, a), a, x) : V::nan_first(V::add(x, a), x, a);
+        case MI_OP_PROD: return ACC32 ? V::nan_first(V::mul(x, a), a, x) : V::nan_first(V::mul(x, a), x, a);
         // MINPS(in, inout) | std::min(in, inout) == MINPS(inout, in)
         case MI_OP_MIN: return INOUT_FIRST ? V::min(x, a) : V::min(a, x);
         default: return INOUT_FIRST ? V::max(x, a) : V::max(a, x);
@@ -58,7 +61,7 @@ inline void lp_group(const uint16_t* const* src, int k, size_t i, uint16_t* dst)
     typename V::F acc = C::load(src[0] + i);
     for (int j = 1; j < k; j++) {
         if (!ACC32 && j > 1) acc = C::round_trip(acc);  // the previous step's storage rounding
-        acc = vop<V, OP, INOUT_FIRST>(C::load(src[j] + i), acc);
+        acc = vop<V, OP, INOUT_FIRST, ACC32>(C::load(src[j] + i), acc);
     }
     V::store(dst + i, LpConv<V, BF, OUT_RNE>::store_bits(acc));
 }

@@ -159,18 +159,31 @@ struct Conv<fp16_t> {
 };
 
 // ---- the operator: acc' = op(in, acc) -----------------------------------------
-// x86 ADDPS/MULPS(in, acc) NaN rule: a NaN operand comes back quieted, `in`
-// first; an invalid operation on non-NaN operands yields the C result (the
-// default NaN on x86).
-inline float nan_first(float r, float in, float acc) {
-    const uint32_t ui = f2u(in), ua = f2u(acc);
-    const bool ni = (ui & 0x7FFFFFFFu) > 0x7F800000u, na = (ua & 0x7FFFFFFFu) > 0x7F800000u;
-    return ni ? u2f(ui | 0x400000u) : (na ? u2f(ua | 0x400000u) : r);
+// x86 ADDPS/MULPS(first, second) NaN rule: a NaN operand comes back
+// quieted, `first`'s when both are; an invalid operation on non-NaN operands
+// yields the C result (the default NaN on x86).  The compiler may swap the
+// operands of a commutative + or *, so the choice is made explicit:
+//   bf16/fp16 steps     first = in   (_mm512_add_ps(in, inout), bf16_intrisics.cpp:20-26)
+//   float/double, and   first = acc  (CCL_REDUCE's `inout op= in` as the reference's
+//   fp32 accumulation            Release build compiles it: tests/golden/ref_comp_vectors.npz)
+template <typename C>
+inline C nan_first(C r, C first, C second) {
+    typedef typename std::conditional<sizeof(C) == 4, uint32_t, uint64_t>::type U;
+    const U q = sizeof(C) == 4 ? (U)0x400000u : (U)0x8000000000000ull;
+    U f, s;
+    memcpy(&f, &first, sizeof f);
+    memcpy(&s, &second, sizeof s);
+    U o = f;
+    if (second != second) o = s | q;
+    if (first != first) o = f | q;
+    C out;
+    memcpy(&out, &o, sizeof out);
+    return (first != first || second != second) ? out : r;
 }
 
 // integers: CCL_REDUCE's wrap-around sum/prod (computed unsigned) and
 // std::min/std::max(in, inout)
-template <int OP, bool INOUT_FIRST, bool LP, typename C>
+template <int OP, bool INOUT_FIRST, bool IN_FIRST, typename C>
 inline C op1_impl(C x, C a, std::true_type) {
     typedef typename std::make_unsigned<C>::type U;
     return OP == MI_OP_SUM ? (C)(U)((U)a + (U)x)
@@ -178,25 +191,27 @@ inline C op1_impl(C x, C a, std::true_type) {
          : OP == MI_OP_MIN ? ((a < x) ? a : x)
                            : ((x < a) ? a : x);
 }
-// floating point: std::min/max(in, inout) or MINPS/MAXPS(in, inout)
-template <int OP, bool INOUT_FIRST, bool LP, typename C>
+// floating point: std::min/max(in, inout) or MINPS/MAXPS(in, inout); sum
+// and prod with the NaN rule above (IN_FIRST: a bf16/fp16 step in storage
+// precision; otherwise the accumulator's NaN wins)
+template <int OP, bool INOUT_FIRST, bool IN_FIRST, typename C>
 inline C op1_impl(C x, C a, std::false_type) {
     C r;
     if (OP == MI_OP_SUM) r = a + x;
     else if (OP == MI_OP_PROD) r = a * x;
     else if (OP == MI_OP_MIN) r = INOUT_FIRST ? ((x < a) ? x : a) : ((a < x) ? a : x);
     else r = INOUT_FIRST ? ((x > a) ? x : a) : ((x < a) ? a : x);
-    if (LP && (OP == MI_OP_SUM || OP == MI_OP_PROD)) r = nan_first((float)r, (float)x, (float)a);
+    if (OP == MI_OP_SUM || OP == MI_OP_PROD) r = IN_FIRST ? nan_first(r, x, a) : nan_first(r, a, x);
     return r;
 }
-template <int OP, bool INOUT_FIRST, bool LP, typename C>
+template <int OP, bool INOUT_FIRST, bool IN_FIRST, typename C>
 inline C op1(C x, C a) {
-    return op1_impl<OP, INOUT_FIRST, LP>(x, a, std::is_integral<C>());
+    return op1_impl<OP, INOUT_FIRST, IN_FIRST>(x, a, std::is_integral<C>());
 }
 
-template <int OP, bool INOUT_FIRST, bool LP, typename C>
+template <int OP, bool INOUT_FIRST, bool IN_FIRST, typename C>
 inline void apply(const C* in, C* acc, size_t n) {
-    for (size_t i = 0; i < n; i++) acc[i] = op1<OP, INOUT_FIRST, LP>(in[i], acc[i]);
+    for (size_t i = 0; i < n; i++) acc[i] = op1<OP, INOUT_FIRST, IN_FIRST>(in[i], acc[i]);
 }
 
 // out = fold(inputs[0..k-1]), blockwise
@@ -238,7 +253,8 @@ void fold(const void* const* inputs, int k, void* out, size_t count, unsigned v)
         Conv<Tag>::widen_(static_cast<const S*>(inputs[0]) + b, acc, n);
         for (int j = 1; j < k; j++) {
             Conv<Tag>::widen_(static_cast<const S*>(inputs[j]) + b, x, n);
-            apply<OP, INOUT_FIRST, HT<Tag>::lp>(x, acc, n);
+            if (acc32) apply<OP, INOUT_FIRST, false>(x, acc, n);  // fp32 accumulation: CCL_REDUCE(float) order
+            else apply<OP, INOUT_FIRST, HT<Tag>::lp>(x, acc, n);
             if (lp && !acc32) {  // round to storage after every step (chained calls)
                 Conv<Tag>::narrow_(acc, tmp, n, vstep, b, trunc_from);
                 Conv<Tag>::widen_(tmp, acc, n);

@@ -155,6 +155,16 @@ __device__ __forceinline__ float x86_nan_first(float r, float first, float secon
     u = nan_bits(a) ? (a | 0x400000u) : u;
     return __uint_as_float(u);
 }
+// The same rule for fp64 (default NaN 0xFFF8000000000000).
+__device__ __forceinline__ bool nan_bits64(uint64_t u) { return (u & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull; }
+__device__ __forceinline__ double x86_nan_first(double r, double first, double second) {
+    const uint64_t a = __double_as_longlong(first), b = __double_as_longlong(second);
+    uint64_t u = __double_as_longlong(r);
+    u = nan_bits64(u) ? 0xFFF8000000000000ull : u;
+    u = nan_bits64(b) ? (b | 0x8000000000000ull) : u;
+    u = nan_bits64(a) ? (a | 0x8000000000000ull) : u;
+    return __longlong_as_double(u);
+}
 
 template <typename Tag>
 __device__ __forceinline__ typename Tr<Tag>::C widen(typename Tr<Tag>::S s) {
@@ -220,11 +230,20 @@ __device__ __forceinline__ C apply(C in, C acc) {
     }
 }
 
-// one fold step in the variant's precision (X: x86 NaN bits, see above)
+// one fold step in the variant's precision (X: x86 NaN bits, see above).
+// Which operand is the first source: a bf16/fp16 step in storage precision
+// is _mm512_add_ps(in, inout) -> `in`; CCL_REDUCE's `inout op= in` on
+// float/double, and the fp32 accumulation of keep-precision (CCL_REDUCE(float),
+// comp.cpp:223-229), compile to ADDPS/MULPS with `inout` first -> the
+// accumulator (pinned by the reference's compiled comp.cpp,
+// tests/golden/ref_comp_vectors.npz).
 template <typename Tag, int OP, unsigned V, bool X = true>
 __device__ __forceinline__ typename Tr<Tag>::C step(typename Tr<Tag>::C x, typename Tr<Tag>::C acc) {
     auto c = apply<OP, (V & V_INOUT_FIRST) != 0>(x, acc);
-    if constexpr (X && Tr<Tag>::lp && (OP == OP_SUM || OP == OP_PROD)) c = x86_nan_first(c, x, acc);
+    if constexpr (X && Tr<Tag>::fp && (OP == OP_SUM || OP == OP_PROD)) {
+        if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) c = x86_nan_first(c, x, acc);
+        else c = x86_nan_first(c, acc, x);
+    }
     if constexpr (Tr<Tag>::lp && !(V & V_ACC_FP32)) c = widen<Tag>(narrow<Tag, V, X>(c));
     return c;
 }
@@ -303,14 +322,17 @@ struct alignas(16) Pack {
 // ---------------------------------------------------------------------------
 template <typename Tag>
 __device__ __forceinline__ uint32_t inf_nan_word(uint32_t w) {
-    // per 16-bit half (bf16, fp16) or per word (fp32): exponent field + one
-    // ulp of it carries into the top bit exactly when the field is all ones
+    // per 16-bit half (bf16, fp16), per word (fp32) or per high word (fp64):
+    // exponent field + one ulp of it carries into the top bit exactly when
+    // the field is all ones
     if constexpr (std::is_same<Tag, bf16_tag>::value) return (w & 0x7F807F80u) + 0x00800080u;
     else if constexpr (std::is_same<Tag, fp16_tag>::value) return (w & 0x7C007C00u) + 0x04000400u;
+    else if constexpr (std::is_same<Tag, double>::value) return (w & 0x7FF00000u) + 0x00100000u;
     else return (w & 0x7F800000u) + 0x00800000u;
 }
 template <typename Tag>
 __device__ __forceinline__ uint32_t inf_nan_bits(u32x4 v) {
+    if constexpr (std::is_same<Tag, double>::value) return inf_nan_word<Tag>(v.y) | inf_nan_word<Tag>(v.w);
     return inf_nan_word<Tag>(v.x) | inf_nan_word<Tag>(v.y) | inf_nan_word<Tag>(v.z) | inf_nan_word<Tag>(v.w);
 }
 template <typename Tag>
@@ -344,8 +366,12 @@ __device__ __forceinline__ u32x4 fold_vec(const u32x4 (&x)[KMAX], int k, uint64_
     return __builtin_bit_cast(u32x4, pr);
 }
 
-// r = the fast fold of x; low precision: refold with the fix-ups when the
-// screen hits (a no-op for other types)
+// r = the fast fold of x; refold with the fix-ups when the screen hits.
+// Low precision: screen the inputs (and a K-input product's result).
+// float / double sum and prod: a NaN operand or an invalid operation makes
+// the result NaN, and a NaN stays NaN along the fold, so the result's own
+// screen (~2 integer ops per dword) finds every row to fix.  Other types and
+// ops: a no-op.
 template <typename Tag, int OP, unsigned V, int KMAX>
 __device__ __forceinline__ u32x4 x86_refold(u32x4 r, const u32x4 (&x)[KMAX], int k, uint64_t e0,
                                             uint64_t trunc_from) {
@@ -356,6 +382,9 @@ __device__ __forceinline__ u32x4 x86_refold(u32x4 r, const u32x4 (&x)[KMAX], int
             if (i < k) bits |= inf_nan_bits<Tag>(x[i]);
         if constexpr (OP == OP_PROD && KMAX > 2) bits |= inf_nan_bits<Tag>(r);
         if (__builtin_expect(inf_nan_hit<Tag>(bits), 0)) r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
+    } else if constexpr (Tr<Tag>::fp && (OP == OP_SUM || OP == OP_PROD)) {
+        if (__builtin_expect(inf_nan_hit<Tag>(inf_nan_bits<Tag>(r)), 0))
+            r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
     }
     return r;
 }

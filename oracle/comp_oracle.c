@@ -3,13 +3,21 @@
  *
  * A plain-C restatement of oneCCL's CPU local reduction, src/comp
  * (reference snapshot 2024-12-20, v2021.14.0).  Every function cites the
- * reference file:line it restates.  The reference's own sources are not
- * buildable here under this project's rules (src/comp/comp.cpp includes
- * common/global/global.hpp, which needs the cmake-generated
- * oneapi/ccl/config.h and the whole library: hwloc, ITT, ATL), so the x86
- * intrinsics it calls are restated from their published (Intel SDM)
- * definitions; oracle/isa_check.c cross-checks those restatements against
- * the real instructions on CPUs that have them.
+ * reference file:line it restates.  The x86 intrinsics the reference calls
+ * are restated from their published (Intel SDM) definitions;
+ * oracle/isa_check.c cross-checks those restatements against the real
+ * instructions on CPUs that have them.
+ *
+ * Pinned to the reference's own compiled code (oracle/Makefile, target ref):
+ *   - oracle/ref_harness.cpp: the AVX-512 bf16 / fp16 bodies
+ *     (src/comp/{bf16,fp16}/*_intrisics.*) -> tests/golden/ref_vectors*.npz;
+ *   - oracle/ref_comp_harness.cpp: src/comp/comp.cpp, bf16/bf16.cpp and the
+ *     logger/datatype sources they need, built with the reference's Release
+ *     flags (ITT off) -> tests/golden/ref_comp_vectors.npz (CCL_REDUCE for the
+ *     ten non-LP types, the scalar bf16 impl, the storage-precision batch
+ *     reduce).  Only ccl::global_data::get/env stay unresolved (the
+ *     runtime's global state), so the LP dispatchers and the keep-precision
+ *     batch reduce, which call them, are pinned through their parts.
  *
  * Build: oracle/Makefile -> oracle/lib/libcomp_oracle.so  (gcc -O3, no
  * -ffast-math, no FMA contraction concerns: each element is one op).
@@ -142,14 +150,35 @@ uint16_t orc_fp32_to_fp16_rne(float f) {
         }                                                                              \
     } while (0)
 
-#define ORC_REDUCE_FP(T)                                                               \
+/* Floating point: `inout op= in` as the reference's Release build (g++ -O3)
+ * compiles it, SSE ADDPS/MULPS with `inout` as the first source: a NaN operand
+ * comes back quieted, inout's when both are; an invalid operation (inf - inf,
+ * 0 * inf) gives the x86 default NaN (sign set).  Written out (NAN_IO_F/D)
+ * rather than left to this compiler's operand order.  Pinned bit for bit,
+ * payloads included, by tests/golden/ref_comp_vectors.npz (the reference's
+ * compiled comp.cpp, oracle/ref_comp_harness.cpp). */
+static inline float nan_io_f(float r, float io, float in) {
+    if (io != io) return u2f(f2u(io) | 0x400000u);
+    if (in != in) return u2f(f2u(in) | 0x400000u);
+    if (r != r) return u2f(0xFFC00000u);
+    return r;
+}
+static inline double nan_io_d(double r, double io, double in) {
+    uint64_t u;
+    if (io != io) { memcpy(&u, &io, 8); u |= 0x8000000000000ull; memcpy(&r, &u, 8); return r; }
+    if (in != in) { memcpy(&u, &in, 8); u |= 0x8000000000000ull; memcpy(&r, &u, 8); return r; }
+    if (r != r) { u = 0xFFF8000000000000ull; memcpy(&r, &u, 8); }
+    return r;
+}
+
+#define ORC_REDUCE_FP(T, NAN_IO)                                                       \
     do {                                                                               \
         const T* a = (const T*)in_buf;                                                 \
         T* b = (T*)inout_buf;                                                          \
         size_t i;                                                                      \
         switch (op) {                                                                  \
-            case OP_SUM: for (i = 0; i < n; i++) b[i] += a[i]; break;                  \
-            case OP_PROD: for (i = 0; i < n; i++) b[i] *= a[i]; break;                 \
+            case OP_SUM: for (i = 0; i < n; i++) b[i] = NAN_IO(b[i] + a[i], b[i], a[i]); break; \
+            case OP_PROD: for (i = 0; i < n; i++) b[i] = NAN_IO(b[i] * a[i], b[i], a[i]); break; \
             case OP_MIN:                                                               \
                 for (i = 0; i < n; i++) b[i] = (b[i] < a[i]) ? b[i] : a[i];            \
                 break;                                                                 \
@@ -184,6 +213,18 @@ static inline float lp_apply(int op, int simd, float in, float io) {
     switch (op) {
         case OP_SUM: return x86_nan_first(in + io, in, io);
         case OP_PROD: return x86_nan_first(in * io, in, io);
+        case OP_MIN: return simd ? ((in < io) ? in : io) : ((io < in) ? io : in);
+        default: return simd ? ((in > io) ? in : io) : ((in < io) ? io : in);
+    }
+}
+
+/* The fp32 accumulation of an fp32-accumulating fan-in: CCL_REDUCE(float)'s
+ * step (keep-precision runs ccl_comp_reduce_regular on float32,
+ * comp.cpp:223-229), so the accumulator's NaN wins a sum or product. */
+static inline float acc32_apply(int op, int simd, float in, float io) {
+    switch (op) {
+        case OP_SUM: return nan_io_f(io + in, io, in);
+        case OP_PROD: return nan_io_f(io * in, io, in);
         case OP_MIN: return simd ? ((in < io) ? in : io) : ((io < in) ? io : in);
         default: return simd ? ((in > io) ? in : io) : ((in < io) ? io : in);
     }
@@ -257,8 +298,8 @@ int orc_comp_reduce(const void* in_buf, size_t n, void* inout_buf, size_t* out_c
         case DT_FLOAT16:
             if (out_count) *out_count = n;
             return orc_fp16_reduce(in_buf, n, inout_buf, op, fp16_impl);
-        case DT_FLOAT32: ORC_REDUCE_FP(float); break;
-        case DT_FLOAT64: ORC_REDUCE_FP(double); break;
+        case DT_FLOAT32: ORC_REDUCE_FP(float, nan_io_f); break;
+        case DT_FLOAT64: ORC_REDUCE_FP(double, nan_io_d); break;
         case DT_BFLOAT16:
             if (out_count) *out_count = n;
             return orc_bf16_reduce(in_buf, n, inout_buf, op, bf16_impl);
@@ -407,7 +448,7 @@ int orc_lp_fanin_acc_fp32(const void* const* inputs, int k, void* out, size_t co
         for (int j = 1; j < k; j++) {
             uint16_t vj = ((const uint16_t*)inputs[j])[i];
             float x = bf ? orc_bf16_to_fp32(vj) : orc_fp16_to_fp32(vj);
-            acc = lp_apply(op, minmax_inout_first, x, acc);
+            acc = acc32_apply(op, minmax_inout_first, x, acc);
         }
         ((uint16_t*)out)[i] = bf ? (bf16_rne ? orc_fp32_to_bf16_rne(acc)
                                              : orc_fp32_to_bf16_trunc(acc))

@@ -207,7 +207,7 @@ def test_batch_reduce_keep_precision(bimpl, k, n):
     arr = _lib.void_ptr_array([p for _, p in holders])
     _lib.check(_lib.mi().mi_reduce_multi(arr, k, holders[0][1], n, BF16, op, flags, _stream()))
     _sync()
-    assert_same(from_dev(holders[0][0], ins[0]), exp, BF16, nan_payload=False)  # util.KEEP_PRECISION_NAN
+    assert_same(from_dev(holders[0][0], ins[0]), exp, BF16)
 
 
 def test_pageable_pointer_refused_without_fault():

@@ -228,7 +228,7 @@ def test_comp_batch_reduce(keep, k, dt):
     oc_ref = oracle.batch_reduce(packed, offsets, n, exp, dt, 0, keep, b_impl, f_impl)
     got = ins[0].copy()
     oc = comp.comp_batch_reduce(ptr(packed), offsets, n, ptr(got), comp.datatype(dt), comp.reduction.sum, keep)
-    assert_same(got, exp, dt, nan_payload=False if keep else None)  # util.KEEP_PRECISION_NAN
+    assert_same(got, exp, dt)
     assert oc == oc_ref
 
 
@@ -749,7 +749,7 @@ def test_keep_precision_past_16_inputs(where, k, op):
         pp, po = ptr(packed), ptr(host)
     oc = comp.comp_batch_reduce(pp, offsets, n, po, comp.datatype.bfloat16, comp.reduction(op), 1)
     got = from_dev(to, exp) if where == "device" else host
-    assert_same(got, exp, BF16, f"k={k}", nan_payload=False)  # util.KEEP_PRECISION_NAN
+    assert_same(got, exp, BF16, f"k={k}")
     assert oc is None  # float32 CCL_REDUCE steps never write out_count
 
 

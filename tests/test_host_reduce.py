@@ -100,7 +100,7 @@ def test_host_keep_precision_matches_batch_reduce(bimpl, k, n):
     oracle.batch_reduce(np.concatenate(ins), [j * n for j in range(k)], n, exp, BF16, 0, 1, bimpl, 0)
     flags = F_ACC_FP32 | ((F_BF16_RNE | F_BF16_TAIL_TRUNC16) if bimpl == oracle.BF16_AVX512BF else 0)
     out = ins[0].copy()
-    assert_same(host_fold(ins, BF16, 0, flags, out), exp, BF16, nan_payload=False)  # util.KEEP_PRECISION_NAN
+    assert_same(host_fold(ins, BF16, 0, flags, out), exp, BF16)
 
 
 @pytest.mark.parametrize("c", refvec.reduce_cases(), ids=lambda c: c["key"])
