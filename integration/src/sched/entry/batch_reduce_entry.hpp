@@ -15,7 +15,10 @@
  * slot and is not read (src/comp/comp.cpp:216-245).  The request is started
  * in start() and polled in update(), like reduce_local_entry's device path
  * (reduce_local_entry.cpp:116-131), so the worker progresses other entries
- * meanwhile.  C++11, as the rest of src/ (CMakeLists.txt:172).
+ * meanwhile -- when the entry is a barrier (sched->add_barrier() after it, as
+ * 0004 does), the only case in which the progress loop holds back the entries
+ * that read its result (sched.cpp:485).  Otherwise it completes in start().
+ * C++11, as the rest of src/ (CMakeLists.txt:172).
  */
 #pragma once
 
@@ -87,6 +90,15 @@ public:
                                     &context,
                                     0, /* bf16_keep_precision_mode */
                                     &req);
+        if (!is_barrier()) {
+            // only a barrier entry holds back the entries after it
+            // (sched.cpp:485): without one, finish here (0004 adds one)
+            ccl_comp_request_wait(req);
+            ccl_comp_request_free(req);
+            req = nullptr;
+            status = ccl_sched_entry_status_complete;
+            return;
+        }
         status = ccl_sched_entry_status_started;
         update();
     }
