@@ -398,14 +398,14 @@ unsigned canon(int dt, int op, unsigned f, int k) {
         case MI_FLOAT64: return mm ? (f & MI_F_MINMAX_INOUT_FIRST) : 0u;
         case MI_FLOAT16: {
             unsigned v = (mm ? (f & (MI_F_MINMAX_INOUT_FIRST | MI_F_FP16_NATIVE_MINMAX)) : 0u) | (f & MI_F_ACC_FP32);
-            if (k <= 2) v &= ~MI_F_ACC_FP32;
+            if (k <= 1 || (k == 2 && mm)) v &= ~MI_F_ACC_FP32;  // a sum/prod step keeps its NaN order
             return v;
         }
         case MI_BFLOAT16: {
             unsigned v = (mm ? (f & MI_F_MINMAX_INOUT_FIRST) : 0u) |
                          (f & (MI_F_BF16_RNE | MI_F_ACC_FP32 | MI_F_BF16_TAIL_TRUNC16));
             if (!((v & MI_F_ACC_FP32) && (v & MI_F_BF16_RNE))) v &= ~MI_F_BF16_TAIL_TRUNC16;
-            if (k == 2 && !(v & MI_F_BF16_TAIL_TRUNC16)) v &= ~MI_F_ACC_FP32;
+            if (k == 2 && mm && !(v & MI_F_BF16_TAIL_TRUNC16)) v &= ~MI_F_ACC_FP32;
             return v;
         }
         default: return 0u;

@@ -132,13 +132,17 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
         case MI_FLOAT64: return mm ? (f & V_INOUT_FIRST) : 0u;
         case MI_FLOAT16: {
             unsigned v = (mm ? (f & (V_INOUT_FIRST | V_FP16_NATIVE)) : 0u) | (f & V_ACC_FP32);
-            if (k <= 2) v &= ~V_ACC_FP32;  // one step: same single rounding
+            // One step rounds once either way, but a sum/prod step with fp32
+            // accumulation takes the accumulator's NaN first (CCL_REDUCE(float)
+            // order), a storage-precision step `in`'s: only min/max (and k = 1,
+            // no step) may drop the bit.
+            if (k <= 1 || (k == 2 && mm)) v &= ~V_ACC_FP32;
             return v;
         }
         case MI_BFLOAT16: {
             unsigned v = (mm ? (f & V_INOUT_FIRST) : 0u) | (f & (V_BF16_RNE | V_ACC_FP32 | V_TAIL_TRUNC));
             if (!((v & V_ACC_FP32) && (v & V_BF16_RNE))) v &= ~V_TAIL_TRUNC;
-            if (k == 2 && !(v & V_TAIL_TRUNC)) v &= ~V_ACC_FP32;
+            if (k == 2 && mm && !(v & V_TAIL_TRUNC)) v &= ~V_ACC_FP32;  // see fp16 above
             return v;
         }
         default: return 0u;  // integers: no variants

@@ -370,8 +370,9 @@ __device__ __forceinline__ u32x4 fold_vec(const u32x4 (&x)[KMAX], int k, uint64_
 // Low precision: screen the inputs (and a K-input product's result).
 // float / double sum and prod: a NaN operand or an invalid operation makes
 // the result NaN, and a NaN stays NaN along the fold, so the result's own
-// screen (~2 integer ops per dword) finds every row to fix.  Other types and
-// ops: a no-op.
+// screen finds every row to fix: one unordered compare per element (an
+// integer exponent screen cost C2 ~3 %, profiles/round3_run2).  Other types
+// and ops: a no-op.
 template <typename Tag, int OP, unsigned V, int KMAX>
 __device__ __forceinline__ u32x4 x86_refold(u32x4 r, const u32x4 (&x)[KMAX], int k, uint64_t e0,
                                             uint64_t trunc_from) {
@@ -383,8 +384,12 @@ __device__ __forceinline__ u32x4 x86_refold(u32x4 r, const u32x4 (&x)[KMAX], int
         if constexpr (OP == OP_PROD && KMAX > 2) bits |= inf_nan_bits<Tag>(r);
         if (__builtin_expect(inf_nan_hit<Tag>(bits), 0)) r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
     } else if constexpr (Tr<Tag>::fp && (OP == OP_SUM || OP == OP_PROD)) {
-        if (__builtin_expect(inf_nan_hit<Tag>(inf_nan_bits<Tag>(r)), 0))
-            r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
+        // unordered self-compares: one v_cmp_u per element pair into a lane mask
+        const Pack<Tag> p = __builtin_bit_cast(Pack<Tag>, r);
+        bool nan = false;
+#pragma unroll
+        for (int e = 0; e < 16 / (int)sizeof(Tag); e++) nan |= (p.e[e] != p.e[e]);
+        if (__builtin_expect(nan, 0)) r = fold_vec<Tag, OP, V, true, KMAX>(x, k, e0, trunc_from);
     }
     return r;
 }
@@ -393,6 +398,38 @@ template <typename Tag, int OP, unsigned V, int KMAX>
 __device__ __forceinline__ u32x4 fold_vec_x86(const u32x4 (&x)[KMAX], int k, uint64_t e0, uint64_t trunc_from) {
     return x86_refold<Tag, OP, V, KMAX>(fold_vec<Tag, OP, V, false, KMAX>(x, k, e0, trunc_from), x, k, e0,
                                         trunc_from);
+}
+
+template <typename Tag>
+__device__ __forceinline__ bool row_has_nan(u32x4 r) {
+    const Pack<Tag> p = __builtin_bit_cast(Pack<Tag>, r);
+    bool nan = false;
+#pragma unroll
+    for (int e = 0; e < 16 / (int)sizeof(Tag); e++) nan |= (p.e[e] != p.e[e]);
+    return nan;
+}
+
+// fold_vec_x86 for the lean kernels.  float / double sum and prod: the rare
+// NaN row re-reads its inputs (`reload(y)`) instead of keeping x live past the
+// fold; kept live, they made the compiler split the guarded load / add / store
+// row into three exec-masked blocks and cost the C2 kernel ~3 %
+// (profiles/round3_run2).  The compiler barrier stops the re-read from being
+// folded into the first read.  Other types: fold_vec_x86.
+template <typename Tag, int OP, unsigned V, int KMAX, typename Reload>
+__device__ __forceinline__ u32x4 fold_row(const u32x4 (&x)[KMAX], int k, uint64_t e0, uint64_t trunc_from,
+                                          Reload&& reload) {
+    if constexpr (!Tr<Tag>::lp && Tr<Tag>::fp && (OP == OP_SUM || OP == OP_PROD)) {
+        u32x4 r = fold_vec<Tag, OP, V, false, KMAX>(x, k, e0, trunc_from);
+        if (__builtin_expect(row_has_nan<Tag>(r), 0)) {
+            asm volatile("" ::: "memory");
+            u32x4 y[KMAX];
+            reload(y);
+            r = fold_vec<Tag, OP, V, true, KMAX>(y, k, e0, trunc_from);
+        }
+        return r;
+    } else {
+        return fold_vec_x86<Tag, OP, V, KMAX>(x, k, e0, trunc_from);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -671,7 +708,10 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
         const uint64_t v = v0 + (uint64_t)j * B;
         if (full || v < a.nvec) {
             const u32x4 xs[2] = {x[j], y[j]};
-            vstore<3>(po + v, fold_vec_x86<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from));
+            vstore<3>(po + v, fold_row<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from, [&](u32x4 (&r)[2]) {
+                          r[0] = vload<3>(p0 + v);
+                          r[1] = vload<3>(p1 + v);
+                      }));
         }
     }
 }
@@ -774,7 +814,11 @@ __global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
             u32x4 xs[K];
 #pragma unroll
             for (int i = 0; i < K; i++) xs[i] = x[i][j];
-            vstore<3>(po + v, fold_vec_x86<Tag, OP, V, K>(xs, K, a.head + v * N, a.trunc_from));
+            vstore<3>(po + v, fold_row<Tag, OP, V, K>(xs, K, a.head + v * N, a.trunc_from, [&](u32x4 (&r)[K]) {
+#pragma unroll
+                          for (int i = 0; i < K; i++)
+                              r[i] = vload<3>(reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in[i]) + hb) + v);
+                      }));
         }
     }
 }
@@ -878,8 +922,15 @@ __global__ __launch_bounds__(B) void reduce2b_kernel(R2Args a) {
     const u32x4 xs[2] = {__builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.acc, byte0, bytes), off, 0, kAuxNT),
                          __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in, byte0, bytes), off, 0, kAuxNT)};
     const uint64_t e0 = a.head + (t0 + threadIdx.x) * N;
-    __builtin_amdgcn_raw_buffer_store_b128(fold_vec_x86<Tag, OP, V, 2>(xs, 2, e0, a.trunc_from),
-                                           tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        fold_row<Tag, OP, V, 2>(xs, 2, e0, a.trunc_from,
+                                [&](u32x4 (&r)[2]) {
+                                    r[0] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.acc, byte0, bytes), off, 0,
+                                                                                 kAuxNT);
+                                    r[1] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in, byte0, bytes), off, 0,
+                                                                                 kAuxNT);
+                                }),
+        tile_rsrc(a.out, byte0, bytes), off, 0, kAuxNT);
 }
 
 // ---------------------------------------------------------------------------

@@ -48,13 +48,14 @@ def test_kernel_matches_reference_code(c, variant):
     n = _count(c)
     ta, pa = to_dev(c["a"], offset_elems=1 if variant == "misaligned" else 0)
     tb, pb = to_dev(c["b"])
-    prev = m.mi_set_max_blocks(2) if variant == "gridcap" else None
+    if variant == "gridcap":
+        _lib.check(m.mi_set_max_blocks(2))  # the general grid-stride kernel
     try:
         _lib.check(m.mi_reduce(pa, pb, n, c["dtype"], c["op"], 0, _stream()))
         torch.cuda.synchronize()
     finally:
-        if prev is not None:
-            m.mi_set_max_blocks(prev)
+        if variant == "gridcap":
+            _lib.check(m.mi_set_max_blocks(0))
     assert_same(from_dev(tb, c["b"]), c["expected"], c["dtype"], c["key"])
 
 

@@ -108,6 +108,30 @@ def test_dropin_host_fanin_matches_reference_batch(c):
     del es
 
 
+@pytest.mark.parametrize("dt,flags", [(11, 0x4 | 0x2), (11, 0x4), (8, 0x4)], ids=["bf16-rne", "bf16-trunc", "fp16"])
+@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("op", [0, 1])
+def test_dropin_host_acc32_nan_order(dt, flags, k, op):
+    """fp32 accumulation (keep-precision, MI_F_ACC_FP32) takes the
+    accumulator's NaN first (CCL_REDUCE(float), pinned by the fixture's float
+    cases), also at k = 2, where one step rounds once either way but the NaN
+    order differs from a storage-precision step."""
+    if not _host_supported():
+        pytest.skip("no AVX2/F16C")
+    rng = np.random.default_rng(k * 10 + op)
+    n = 4099
+    nan = (0x7F81, 0xFFC3, 0x7FA5) if dt == 11 else (0x7C01, 0xFE03, 0x7E55)
+    ins = []
+    for j in range(k):
+        x = rng.integers(0, 1 << 16, n, dtype=np.uint32).astype(np.uint16)
+        x[j::3] = nan[j % 3]  # overlapping NaN lanes with different payloads
+        ins.append(x)
+    exp = oracle.lp_fanin_acc_fp32(ins, dt, op, bool(flags & 0x2), False)
+    out = np.zeros(n, np.uint16)
+    _host_reduce(ins, out, dt, op, flags)
+    _check(out, exp, f"dt={dt} k={k} op={op}")
+
+
 def test_fixture_covers_every_row():
     got = {(c["kind"], c["dtype"], c["op"]) for k in ("reduce", "reduce1", "bf16s", "batch") for c in refcomp.cases(k)}
     want = {("reduce", dt, op) for dt in (0, 1, 2, 3, 4, 5, 6, 7, 9, 10) for op in range(4)}

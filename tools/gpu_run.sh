@@ -117,6 +117,11 @@ for step in "$@"; do
             run dist2self 300 python bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --no-cpu-baseline ;;
         pmcjson)  # the PMC passes of `pmc` summarised into profiles-ready JSON
             python tools/pmc_traffic.py "$OUT/pmc.json" "c2=$OUT:3221225472" > "$OUT/pmcjson.out" 2>&1 ;;
+        ab)  # A/B of earlier kernel builds against the current one, same box (tools/ab_c2.py)
+            for v in ${AB_VARIANTS:-old}; do
+                run "ab_${v}_${AB_CONFIG:-c2}" 300 python tools/ab_c2.py tools/ab/$v/libmi_reduce.so \
+                    oneccl_amd/lib/libmi_reduce.so --config ${AB_CONFIG:-c2} --rounds ${AB_ROUNDS:-10}
+            done ;;
         sizes)
             run sizes 600 python tools/size_sweep.py ;;
         sizes_fp32)
