@@ -105,11 +105,19 @@ def cpu_baseline(cfg, seconds):
         f = rng.random(n, dtype=np.float32) * 2 - 1
         ins = [oracle.f32_to_bf16(f, True) if dt == 11 else oracle.f32_to_fp16(f) for _ in range(k)]
     acc = ins[0].copy()
+    # the reference's own compiled CCL_REDUCE (oracle/_ref, its Release flags)
+    # when it was built and the type is one it reaches; else the restatement
+    use_ref = oracle.ref_comp_available() and dt not in (8, 11)
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(16)
 
     def one(nthreads):
         t0 = time.perf_counter()
-        for x in ins[1:]:
-            oracle.comp_reduce_mt(x, acc, dt, op, nthreads)  # chained 2-input calls, as the reference
+        for x in ins[1:]:  # chained 2-input calls, as the reference
+            if use_ref:
+                oracle.ref_comp_reduce(x, acc, dt, op, nthreads, pool)
+            else:
+                oracle.comp_reduce_mt(x, acc, dt, op, nthreads)
         return time.perf_counter() - t0
 
     res = {}
@@ -120,6 +128,15 @@ def cpu_baseline(cfg, seconds):
         while len(times) < 3 or (time.perf_counter() - t_start < seconds / 2 and len(times) < 200):
             times.append(one(nthreads))
         res[nthreads] = (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times))
+    pool.shutdown()
+    port_1 = None
+    if use_ref:  # the restatement on the same bucket, one thread, for comparison
+        tp = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            oracle.comp_reduce_mt(ins[1], acc, dt, op, 1)
+            tp.append(time.perf_counter() - t0)
+        port_1 = round(bucket / GiB / min(tp) * (k - 1), 3)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -144,15 +161,18 @@ def cpu_baseline(cfg, seconds):
     copy_gbps = 2 * src.nbytes / min(ct) / 1e9
     del src, dst
     return {
-        "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "reference" if use_ref else "port",
         "traffic_GBps_1core": round(b1 * GiB * (k + 1) / 1e9, 1),
         "copy_probe_GBps_1core": round(copy_gbps, 1),
         "traffic_note": f"the 1-core rate moves (k+1) = {k + 1} bucket-sizes of DRAM traffic per reduce; "
                         "copy_probe = 2 x bytes / time of one single-threaded memcpy of the bucket (read + "
                         "write), measured in the same run as an independent ceiling for one core",
-        "sample": f"oracle/comp_oracle.c (CPU restatement of src/comp CCL_REDUCE loop, gcc -O3) on the same "
-                  f"{bucket // (1 << 20)} MiB bucket x {k}-input, best of {r1} reps (median {m1:.2f} GiB/s); "
-                  f"1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
+        "sample": (("the reference's own ccl_comp_reduce_regular / CCL_REDUCE (src/comp/comp.cpp compiled with its "
+                    "Release flags, g++ -O3, oracle/_ref/libref_ccl_comp.so)") if use_ref else
+                   "oracle/comp_oracle.c (CPU restatement of src/comp CCL_REDUCE loop, gcc -O3)") +
+                  f" on the same {bucket // (1 << 20)} MiB bucket x {k}-input, best of {r1} reps (median {m1:.2f} "
+                  f"GiB/s); 1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
+        "port_1thread": port_1,
         "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": nt, "reps": rn,
                          "note": "range split over threads, emulating CCL_WORKER_COUNT"},
         "cpu_model": cpu_model, "host_cpus": os.cpu_count(),

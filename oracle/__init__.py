@@ -155,3 +155,55 @@ def fp16_to_f32(h: np.ndarray) -> np.ndarray:
     out = np.empty(src.shape, np.float32)
     lib().orc_convert_fp16_to_fp32_arrays(src.ctypes.data, out.ctypes.data, src.size)
     return out
+
+
+# ---- the reference's own compiled CCL_REDUCE (oracle/_ref, built here) ----
+# oracle/_ref/libref_ccl_comp.so = oracle/ref_comp_harness.cpp over the
+# reference's src/comp/comp.cpp & co. with its Release flags (Makefile target
+# refcomp).  Built in the container (needs /root/reference); the built library
+# travels to the GPU box, where bench.py's cpu_baseline leg times it.
+REF_COMP_SO = ODIR / "_ref" / "libref_ccl_comp.so"
+_ref_comp = None
+
+
+def ref_comp_available() -> bool:
+    return REF_COMP_SO.exists()
+
+
+def ref_comp_lib() -> ctypes.CDLL:
+    """Loaded RTLD_LAZY: ccl::global_data::get/env stay unbound and are never
+    called on the paths used (see the harness)."""
+    global _ref_comp
+    if _ref_comp is None:
+        import os
+        L = ctypes.CDLL(str(REF_COMP_SO), mode=os.RTLD_LAZY)
+        L.ref_ccl_comp_reduce_regular.argtypes = [c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_size_t, c_int]
+        L.ref_ccl_comp_reduce_regular.restype = c_int
+        _ref_comp = L
+    return _ref_comp
+
+
+def ref_comp_reduce(in_buf: np.ndarray, inout_buf: np.ndarray, dtype: int, op: int, nthreads: int = 1,
+                    pool=None) -> None:
+    """The reference's ccl_comp_reduce_regular on host arrays (non-LP types),
+    the element range split over `nthreads` threads (ctypes drops the GIL),
+    as CCL_WORKER_COUNT workers would each reduce their chunk."""
+    L = ref_comp_lib()
+    n, es = in_buf.size, in_buf.itemsize
+    if nthreads <= 1:
+        assert L.ref_ccl_comp_reduce_regular(in_buf.ctypes.data, n, inout_buf.ctypes.data, None, dtype, es, op) == 0
+        return
+    per = (n + nthreads - 1) // nthreads
+    parts = [(i * per, min(n, (i + 1) * per)) for i in range(nthreads) if i * per < n]
+
+    def one(se):
+        s, e = se
+        return L.ref_ccl_comp_reduce_regular(in_buf.ctypes.data + s * es, e - s, inout_buf.ctypes.data + s * es,
+                                             None, dtype, es, op)
+
+    if pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(nthreads) as ex:
+            assert all(rc == 0 for rc in ex.map(one, parts))
+    else:
+        assert all(rc == 0 for rc in pool.map(one, parts))

@@ -176,3 +176,22 @@ def test_reference_library_leaves_only_global_state_unbound():
     ours = {u for u in undef if "ccl" in u}
     assert ours == {"ccl::global_data::env()", "ccl::global_data::get()"} | \
         {u for u in ours if u.startswith("ccl::detail::ccl_api_type_attr_traits")}, ours
+
+
+@pytest.mark.skipif(not oracle.ref_comp_available(), reason="oracle/_ref/libref_ccl_comp.so not built")
+@pytest.mark.parametrize("nthreads", [1, 4])
+def test_reference_cpu_baseline_call_matches_oracle(nthreads):
+    """bench.py's cpu_baseline times the reference's own compiled CCL_REDUCE
+    (kind "reference"), range-split over threads: same bits as the oracle."""
+    rng = np.random.default_rng(nthreads)
+    for dt, op in ((9, 0), (4, 3), (6, 1), (10, 2)):
+        if dt in (9, 10):
+            a = rng.standard_normal(100_003).astype(oracle.NP_DTYPE[dt])
+            b = rng.standard_normal(100_003).astype(oracle.NP_DTYPE[dt])
+        else:
+            a = rng.integers(-1000, 1000, 100_003).astype(oracle.NP_DTYPE[dt])
+            b = rng.integers(-1000, 1000, 100_003).astype(oracle.NP_DTYPE[dt])
+        x, y = b.copy(), b.copy()
+        oracle.ref_comp_reduce(a, x, dt, op, nthreads)
+        oracle.comp_reduce(a, y, dt, op)
+        _check(x, y, f"dt={dt} op={op}")
