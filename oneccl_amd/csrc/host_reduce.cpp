@@ -168,17 +168,13 @@ struct Conv<fp16_t> {
 //   fp32 accumulation            Release build compiles it: tests/golden/ref_comp_vectors.npz)
 template <typename C>
 inline C nan_first(C r, C first, C second) {
+    // two selects on the bits: the loops stay vectorized (a memcpy-and-branch
+    // form of this cost the fp32 fold 4x)
     typedef typename std::conditional<sizeof(C) == 4, uint32_t, uint64_t>::type U;
     const U q = sizeof(C) == 4 ? (U)0x400000u : (U)0x8000000000000ull;
-    U f, s;
-    memcpy(&f, &first, sizeof f);
-    memcpy(&s, &second, sizeof s);
-    U o = f;
-    if (second != second) o = s | q;
-    if (first != first) o = f | q;
-    C out;
-    memcpy(&out, &o, sizeof out);
-    return (first != first || second != second) ? out : r;
+    U o = (second != second) ? (__builtin_bit_cast(U, second) | q) : __builtin_bit_cast(U, r);
+    o = (first != first) ? (__builtin_bit_cast(U, first) | q) : o;
+    return __builtin_bit_cast(C, o);
 }
 
 // integers: CCL_REDUCE's wrap-around sum/prod (computed unsigned) and
@@ -214,9 +210,82 @@ inline void apply(const C* in, C* acc, size_t n) {
     for (size_t i = 0; i < n; i++) acc[i] = op1<OP, INOUT_FIRST, IN_FIRST>(in[i], acc[i]);
 }
 
+// ---- float / double sum and product: ADDPS/MULPS (PD) with the accumulator
+// as the first source, as the reference's Release build compiles CCL_REDUCE's
+// `inout op= in` (tests/golden/ref_comp_vectors.npz).  The instruction itself
+// then gives the reference's NaN bits (first NaN operand quieted, the default
+// NaN on an invalid operation); inline asm fixes the operand order, which
+// the compiler may otherwise swap for a commutative + or *.
+template <int OP>
+inline __m256 vop_first(__m256 a, __m256 x) {
+    __m256 r;
+    if (OP == MI_OP_SUM) asm("vaddps %2, %1, %0" : "=x"(r) : "x"(a), "x"(x));
+    else asm("vmulps %2, %1, %0" : "=x"(r) : "x"(a), "x"(x));
+    return r;
+}
+template <int OP>
+inline __m256d vop_first(__m256d a, __m256d x) {
+    __m256d r;
+    if (OP == MI_OP_SUM) asm("vaddpd %2, %1, %0" : "=x"(r) : "x"(a), "x"(x));
+    else asm("vmulpd %2, %1, %0" : "=x"(r) : "x"(a), "x"(x));
+    return r;
+}
+inline __m256 vload(const float* p) { return _mm256_loadu_ps(p); }
+inline __m256d vload(const double* p) { return _mm256_loadu_pd(p); }
+inline void vstore(float* p, __m256 v) { _mm256_storeu_ps(p, v); }
+inline void vstore(double* p, __m256d v) { _mm256_storeu_pd(p, v); }
+
+template <typename C, int OP>
+inline void fp_group(const C* const* in, int k, size_t i, C* out) {  // W elements at i
+    auto acc = vop_first<OP>(vload(in[0] + i), vload(in[1] + i));
+    for (int j = 2; j < k; j++) acc = vop_first<OP>(acc, vload(in[j] + i));
+    vstore(out + i, acc);
+}
+
+template <typename C, int OP>
+void fold_fp(const void* const* inputs, int k, void* out, size_t count) {
+    constexpr size_t W = 32 / sizeof(C);
+    const C* in[MI_MAX_INPUTS];
+    for (int j = 0; j < k; j++) in[j] = static_cast<const C*>(inputs[j]);
+    C* o = static_cast<C*>(out);
+    // Every group reads all its inputs before it stores, so `out` may alias
+    // any input (the same elements of a later input are read first).
+    size_t i = 0;
+    for (; i + W <= count; i += W) fp_group<C, OP>(in, k, i, o);
+    if (i < count) {  // zero-padded last group
+        const size_t r = count - i;
+        alignas(32) C pad[MI_MAX_INPUTS][W] = {};
+        const C* p[MI_MAX_INPUTS] = {};
+        for (int j = 0; j < k; j++) {
+            memcpy(pad[j], in[j] + i, r * sizeof(C));
+            p[j] = pad[j];
+        }
+        alignas(32) C res[W];
+        fp_group<C, OP>(p, k, 0, res);
+        memcpy(o + i, res, r * sizeof(C));
+    }
+}
+
+// float / double sum and product take fold_fp (C++11: no if constexpr in
+// the in-tree build)
+template <typename Tag, int OP,
+          bool FP = std::is_floating_point<Tag>::value && (OP == MI_OP_SUM || OP == MI_OP_PROD)>
+struct FpFold {
+    static bool run(const void* const*, int, void*, size_t) { return false; }
+};
+template <typename Tag, int OP>
+struct FpFold<Tag, OP, true> {
+    static bool run(const void* const* inputs, int k, void* out, size_t count) {
+        if (k < 2) return false;
+        fold_fp<Tag, OP>(inputs, k, out, count);
+        return true;
+    }
+};
+
 // out = fold(inputs[0..k-1]), blockwise
 template <typename Tag, int OP, bool INOUT_FIRST>
 void fold(const void* const* inputs, int k, void* out, size_t count, unsigned v) {
+    if (FpFold<Tag, OP>::run(inputs, k, out, count)) return;
     typedef typename HT<Tag>::S S;
     typedef typename HT<Tag>::C C;
     const bool lp = HT<Tag>::lp;
