@@ -369,3 +369,48 @@ def test_split_start_argument_errors():
                                    ctypes.byref(req)) < 0
     assert m.mi_reduce_split_start(arr, 2, a.ctypes.data, a.size, FP32, 4, 0, -1, 256, _host_fold_ptr(),
                                    ctypes.byref(req)) < 0
+
+
+@pytest.mark.parametrize("where", ["device", "pinned", "pageable"])
+def test_timed_request_reports_its_run_time(where):
+    """mi_reduce_start_timed: the duration measured where the request ran (a
+    HIP event pair around a direct launch, the staging worker's clock for a
+    staged one), within the caller's wall time; ADVICE r2 (the dispatcher's
+    GPU-alone rate).  An untimed direct request has none."""
+    import time
+
+    import torch
+    m = _lib.mi()
+    n = (32 << 20) // 4
+    a = rand_array(FP32, n, seed=5, specials=False)
+    b = rand_array(FP32, n, seed=6, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    if where == "device":
+        ta, pa = to_dev(a)
+        tb, pb = to_dev(b)
+    elif where == "pinned":
+        ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+        pa, pb = ha.data_ptr(), hb.data_ptr()
+    else:
+        hbn = b.copy()
+        pa, pb = a.ctypes.data, hbn.ctypes.data
+    ins = _lib.void_ptr_array([pb, pa])
+    req = ctypes.c_void_p()
+    t0 = time.perf_counter()
+    _lib.check(m.mi_reduce_start_timed(ins, 2, pb, n, FP32, 0, 0, -1, ctypes.byref(req)))
+    _lib.check(m.mi_wait(req))
+    wall = time.perf_counter() - t0
+    t = ctypes.c_double(-1)
+    _lib.check(m.mi_request_run_time(req, ctypes.byref(t)))
+    _lib.check(m.mi_request_free(req))
+    assert 0 < t.value <= wall + 1e-3, (t.value, wall)
+    got = from_dev(tb, b) if where == "device" else (hb.numpy().view(np.float32) if where == "pinned" else hbn)
+    assert_same(got, exp, FP32, where)
+    if where == "device":  # untimed direct request: no run time
+        req2 = ctypes.c_void_p()
+        _lib.check(m.mi_reduce_start(ins, 2, pb, n, FP32, 0, 0, -1, ctypes.byref(req2)))
+        _lib.check(m.mi_wait(req2))
+        assert m.mi_request_run_time(req2, ctypes.byref(t)) != 0
+        _lib.check(m.mi_request_free(req2))

@@ -365,3 +365,27 @@ def test_async_split_adapts_its_share(kind, threshold):
     from oneccl_amd import _lib
     left = ctypes.c_uint(0)
     assert _lib.shim().mi_ccl_comp_split_gpu_rate(1 if kind == "pinned" else 0, ctypes.byref(left)) > 0
+
+
+def test_pinned_zero_sends_pinned_buckets_to_the_gpu_alone(threshold):
+    """CCL_COMP_HOST_MAX_PINNED_BYTES=0: a pinned bucket above
+    the pageable threshold is never split with the CPU (the thread's pinned
+    share is never started); a pageable one still is."""
+    import torch
+    threshold(1 << 20, CCL_COMP_HOST_MAX_PINNED_BYTES=0)
+    n = (24 << 20) // 4 + 7
+    a = rand_array(FP32, n, seed=11, specials=False)
+    b = rand_array(FP32, n, seed=12, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8)
+    ta = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+    tb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+    for _ in range(3):
+        tb.copy_(torch.from_numpy(b.view(np.uint8)))
+        comp.comp_reduce(ta.data_ptr(), n, tb.data_ptr(), comp.datatype.float32, comp.reduction.sum)
+        assert_same(tb.numpy().view(np.float32), exp, FP32, "pinned")
+    assert _split_share(True) < 0  # no split ever started for pinned buckets
+    hb = b.copy()
+    comp.comp_reduce(a.ctypes.data, n, hb.ctypes.data, comp.datatype.float32, comp.reduction.sum)
+    assert_same(hb, exp, FP32, "pageable")
+    assert _split_share(False) >= 0.1  # the pageable bucket was split
