@@ -114,9 +114,11 @@ for step in "$@"; do
             run dist2_strong 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29534 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --scaling strong ;;
         dist2self)  # bench.py as its own launcher: --gpus 2 with no WORLD_SIZE (both ranks share the box's GPU)
-            run dist2self 300 python bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --no-cpu-baseline ;;
-        pmcjson)  # the PMC passes of `pmc` summarised into profiles-ready JSON
-            python tools/pmc_traffic.py "$OUT/pmc.json" "c2=$OUT:3221225472" > "$OUT/pmcjson.out" 2>&1 ;;
+            run dist2self 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline ;;  # nccl -> gloo on 1 GPU
+        pmcjson)  # the PMC passes of `pmc` (and PMC_CONFIG=c4's) summarised into profiles-ready JSON
+            specs="c2=$OUT:3221225472"
+            [ -d "$OUT/pmc_c4" ] && specs="$specs c4=$OUT/pmc_c4:9663676416"
+            python tools/pmc_traffic.py "$OUT/pmc.json" $specs > "$OUT/pmcjson.out" 2>&1 ;;
         ab)  # A/B of earlier kernel builds against the current one, same box (tools/ab_c2.py)
             for v in ${AB_VARIANTS:-old}; do
                 run "ab_${v}_${AB_CONFIG:-c2}" 300 python tools/ab_c2.py tools/ab/$v/libmi_reduce.so \
