@@ -1,9 +1,9 @@
 """Shared helpers for the parity tests: seeded inputs (with the special
-values the reference's semantics distinguish), numpy<->device transfer and
-the comparison rule (bit-exact; bf16/fp16 NaN payloads included, since the
-kernels restate x86's NaN rules for the reference's AVX-512 paths; for fp32
-and fp64, whose reference is a compiler-vectorized C loop with no fixed
-operand order, two NaNs of any payload compare equal)."""
+values the reference's semantics distinguish, NaNs with payloads of both
+signs among them), numpy<->device transfer and the comparison rule
+(bit-exact, NaN payloads included for every type: the kernels and the host
+path restate x86's NaN rules for the reference's AVX-512 paths and for its
+compiled CCL_REDUCE, tests/golden/ref_comp_vectors.npz)."""
 from __future__ import annotations
 
 import numpy as np
@@ -19,9 +19,11 @@ DT_NAME = {0: "int8", 1: "uint8", 2: "int16", 3: "uint16", 4: "int32", 5: "uint3
            8: "float16", 9: "float32", 10: "float64", 11: "bfloat16"}
 OP_NAME = {0: "sum", 1: "prod", 2: "min", 3: "max"}
 
-F32_SPECIALS = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, -np.nan, 1e-40, -1e-40, 1e-45,
-                         3.4e38, -3.4e38, 1.17549435e-38, 65504.0, 6.1e-5, 5.96e-8, 2.0 ** -126],
-                        dtype=np.float32)
+F32_SPECIALS = np.concatenate([
+    np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, -np.nan, 1e-40, -1e-40, 1e-45,
+              3.4e38, -3.4e38, 1.17549435e-38, 65504.0, 6.1e-5, 5.96e-8, 2.0 ** -126], dtype=np.float32),
+    # quiet NaNs with payloads of both signs and a signalling NaN
+    np.array([0x7FC00123, 0xFFC00456, 0x7F800005], dtype=np.uint32).view(np.float32)])
 
 
 def rand_array(dtype: int, n: int, seed: int, op: int = 0, specials: bool = True) -> np.ndarray:
@@ -45,9 +47,12 @@ def rand_array(dtype: int, n: int, seed: int, op: int = 0, specials: bool = True
     if dtype == FP64:
         a = rng.standard_normal(n) * (10.0 ** rng.integers(-3, 4, size=n))
         if specials and n > 40:
-            idx = rng.choice(n, size=len(F32_SPECIALS), replace=False)
-            a[idx] = F32_SPECIALS.astype(np.float64)
+            idx = rng.choice(n, size=len(F32_SPECIALS) + 3, replace=False)
+            with np.errstate(invalid="ignore"):  # the signalling NaN quiets on widening
+                a[idx[:len(F32_SPECIALS)]] = F32_SPECIALS.astype(np.float64)
             a[idx[0]] = 1e-310  # fp64 denormal
+            a.view(np.uint64)[idx[len(F32_SPECIALS):]] = np.array(  # fp64 NaN payloads, both signs, signalling
+                [0x7FF8000000000123, 0xFFF8000000000456, 0x7FF0000000000007], np.uint64)
         return a
     f = (rng.standard_normal(n) * (2.0 ** rng.integers(-8, 9, size=n))).astype(np.float32)
     if specials and n > 40:
