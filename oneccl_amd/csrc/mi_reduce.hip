@@ -735,6 +735,16 @@ struct ThreadCtx {
 thread_local ThreadCtx t_ctx;
 std::once_flag g_exit_hook;
 
+// Register at_process_exit once, after the HIP runtime is initialised (a HIP
+// call first), so that it runs before the runtime's own exit teardown.
+void ensure_exit_hook() {
+    std::call_once(g_exit_hook, [] {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::atexit(at_process_exit);
+    });
+}
+
 int get_ctx(int device, DevCtx** out) {
     if (device < 0) MI_HIP(hipGetDevice(&device));
     if ((size_t)device >= t_ctx.devs.size()) t_ctx.devs.resize(device + 1, nullptr);
@@ -750,7 +760,7 @@ int get_ctx(int device, DevCtx** out) {
             ~Restore() { (void)hipSetDevice(dev); }
         } restore{prev};
         MI_HIP(hipSetDevice(device));
-        std::call_once(g_exit_hook, [] { std::atexit(at_process_exit); });
+        ensure_exit_hook();
         std::unique_ptr<DevCtx> d(new DevCtx());
         d->device = device;
         for (int s = 0; s < 2; s++) MI_HIP(hipStreamCreateWithFlags(&d->stream[s], hipStreamNonBlocking));
@@ -1051,6 +1061,7 @@ struct StageWorker {
     bool stop = false;
 
     void submit(const std::shared_ptr<AsyncJob>& j) {
+        ensure_exit_hook();  // the job's HIP calls are then covered by the exit handler
         {
             std::lock_guard<std::mutex> lk(mu);
             q.push_back(j);
