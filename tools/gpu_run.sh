@@ -103,6 +103,9 @@ for step in "$@"; do
                 --mib ${WORKERS_MIB:-8,64} --modes ${WORKERS_MODES:-oracle,host,split,default} &&
             run workers_pinned 600 python tools/workers_sweep.py --segv-trace --pinned --workers ${WORKERS:-1,2,4,8,16} \
                 --mib ${WORKERS_MIB:-64} --modes ${WORKERS_MODES:-oracle,host,split,default} ;;
+        exittests)  # process exit against thread teardown and un-waited asynchronous requests
+            run pytest_exit 300 python -u -m pytest tests/test_gpu_shim.py -m gpu -q -k exit -p no:cacheprovider \
+                --timeout 120 --timeout-method thread ;;
         dispatchtests)
             run pytest_dispatch 600 python -u -m pytest tests/test_gpu_dispatch.py tests/test_host_reduce.py -m "gpu or not gpu" \
                 -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
