@@ -17,12 +17,13 @@
 // ccl::global_data::env(), whose definition needs the library's global state,
 // logger and hwloc/ITT closure — so this harness calls the per-impl bodies
 // directly with the impl and op chosen by the caller, exactly as the
-// dispatcher would.  Not linkable here (and therefore pinned by the
-// restatement + the survey's probes only): the scalar bf16 impl
-// (bf16.cpp:63-85) and CCL_REDUCE (comp.cpp:31-58) live in translation units
-// that reference CCL_FATAL's logger, and ccl_comp_batch_reduce (comp.cpp:202-249)
-// additionally needs sched/ITT.  AVX512_FP16 native math needs gcc >= 12
-// (reference cmake/helpers.cmake:97-102; gcc 11.4 here), so it is not built.
+// dispatcher would.  The scalar bf16 impl (bf16.cpp:63-85), CCL_REDUCE
+// (comp.cpp:31-58) and ccl_comp_batch_reduce (comp.cpp:202-249) live in
+// translation units that also need the logger and datatype sources; round 3
+// links those from the reference too (oracle/ref_comp_harness.cpp,
+// _ref/libref_ccl_comp.so).  AVX512_FP16 native math needs gcc >= 12
+// (reference cmake/helpers.cmake:97-102; gcc 11.4 here): ref_fp16native.cpp
+// builds it with ROCm's clang++.
 //
 // Nothing in the product (oneccl_amd/, include/) links or loads this.
 #include "comp/bf16/bf16_intrisics.hpp"
