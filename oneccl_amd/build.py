@@ -191,8 +191,11 @@ def build_asan(force: bool = False) -> Path:
 
 def build_oracle(force: bool = False) -> Path:
     """TEST INFRASTRUCTURE: the CPU oracle (oracle/Makefile), and, where the
-    reference tree is present (this container, not the GPU box), the harness
-    over the reference's own bf16/fp16 code (oracle/_ref, `make -C oracle ref`)."""
+    reference tree is present (this container, not the GPU box), the harnesses
+    over the reference's own compiled code (oracle/_ref, `make -C oracle ref`:
+    the AVX-512 bf16/fp16 bodies, the avx512fp16 impl, and src/comp/comp.cpp's
+    CCL_REDUCE / scalar bf16 / batch reduce, whose library also serves as
+    bench.py's CPU baseline)."""
     odir = ROOT / "oracle"
     if force:
         _run(["make", "-C", str(odir), "clean"])
