@@ -195,3 +195,29 @@ def test_reference_cpu_baseline_call_matches_oracle(nthreads):
         oracle.ref_comp_reduce(a, x, dt, op, nthreads)
         oracle.comp_reduce(a, y, dt, op)
         _check(x, y, f"dt={dt} op={op}")
+
+
+@pytest.mark.skipif(not oracle.ref_comp_available(), reason="oracle/_ref/libref_ccl_comp.so not built")
+@pytest.mark.parametrize("nontemporal", [0, 1])
+def test_dropin_copy_matches_reference_copy(nontemporal):
+    """ccl_comp_copy (comp.cpp:60-74, memcpy / memcpy_nontemporal of
+    common/utils/memcpy.cpp): the reference's own compiled copy and the
+    drop-in's (host buffers stay on the calling thread's CPU) give the same
+    bytes for odd sizes at every source/destination misalignment, and touch
+    nothing outside the range."""
+    import ctypes
+    L = oracle.ref_comp_lib()
+    L.ref_ccl_comp_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.ref_ccl_comp_copy.restype = ctypes.c_int
+    s = _lib.shim()
+    rng = np.random.default_rng(nontemporal)
+    src = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    for nbytes in (0, 1, 7, 63, 64, 255, 256, 257, 4099, 40000):
+        for so in (0, 1, 13, 64):
+            for do in (0, 3, 32):
+                a = rng.integers(0, 256, nbytes + 200, dtype=np.uint8)
+                b = a.copy()
+                assert L.ref_ccl_comp_copy(src.ctypes.data + so, a.ctypes.data + do, nbytes, nontemporal) == 0
+                _lib.check_shim(s.mi_ccl_comp_copy(src.ctypes.data + so, b.ctypes.data + do, nbytes, nontemporal),
+                                "ccl_comp_copy")
+                assert np.array_equal(a, b), (nbytes, so, do)
