@@ -3,7 +3,8 @@
 for fp32 sum, int32 max and int64 prod.  Per size: device-resident kernel time
 (hipEvent pair, mean of reps), the synchronous drop-in call on device buffers
 (ccl_comp_reduce path: launch + stream sync, host wall), the host-resident
-call on pinned and pageable buffers, and the CPU oracle on 1 thread.
+call on pinned and pageable buffers, and one CPU thread: the reference's own compiled
+CCL_REDUCE (oracle/_ref) where built, else the oracle.
 One JSON line per (config, size) on stdout.
 
   python tools/size_sweep.py [--max-mib 1024] [--reps 20]
@@ -86,13 +87,23 @@ def main():
                         m.mi_reduce_sync(x, y, n, dt, op, 0, -1)
                         t.append(time.perf_counter() - t0)
                     row[key] = round(min(t) * 1e6, 2)
-                oracle.comp_reduce(pa, pb, dt, op)
+                # one CPU thread: the reference's own compiled CCL_REDUCE where
+                # oracle/_ref was built (it travels with the tree), else the oracle
+                use_ref = oracle.ref_comp_available() and dt not in (8, 11)
+
+                def cpu():
+                    if use_ref:
+                        oracle.ref_comp_reduce(pa, pb, dt, op)
+                    else:
+                        oracle.comp_reduce(pa, pb, dt, op)
+                cpu()
                 t = []
                 for _ in range(max(3, reps // 2)):
                     t0 = time.perf_counter()
-                    oracle.comp_reduce(pa, pb, dt, op)
+                    cpu()
                     t.append(time.perf_counter() - t0)
                 row["cpu_1thread_us"] = round(min(t) * 1e6, 2)
+                row["cpu_1thread_kind"] = "reference" if use_ref else "oracle"
             print(json.dumps(row), flush=True)
             del a, b
             torch.cuda.empty_cache()
