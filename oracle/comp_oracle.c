@@ -10,7 +10,7 @@
  *
  * Pinned to the reference's own compiled code (oracle/Makefile, target ref):
  *   - oracle/ref_harness.cpp: the AVX-512 bf16 / fp16 bodies
- *     (src/comp/{bf16,fp16}/*_intrisics.*) -> tests/golden/ref_vectors*.npz;
+ *     (the _intrisics sources of src/comp/bf16 and src/comp/fp16) -> tests/golden/ref_vectors*.npz;
  *   - oracle/ref_comp_harness.cpp: src/comp/comp.cpp, bf16/bf16.cpp and the
  *     logger/datatype sources they need, built with the reference's Release
  *     flags (ITT off) -> tests/golden/ref_comp_vectors.npz (CCL_REDUCE for the
@@ -157,18 +157,21 @@ uint16_t orc_fp32_to_fp16_rne(float f) {
  * rather than left to this compiler's operand order.  Pinned bit for bit,
  * payloads included, by tests/golden/ref_comp_vectors.npz (the reference's
  * compiled comp.cpp, oracle/ref_comp_harness.cpp). */
+/* (written as selects, lowest priority first, so that gcc keeps the loop
+ * vectorized) */
 static inline float nan_io_f(float r, float io, float in) {
-    if (io != io) return u2f(f2u(io) | 0x400000u);
-    if (in != in) return u2f(f2u(in) | 0x400000u);
-    if (r != r) return u2f(0xFFC00000u);
-    return r;
+    uint32_t o = (r != r) ? 0xFFC00000u : f2u(r);          /* invalid operation: default NaN */
+    o = (in != in) ? (f2u(in) | 0x400000u) : o;             /* else `in`'s NaN, quieted */
+    o = (io != io) ? (f2u(io) | 0x400000u) : o;             /* `inout`'s NaN first */
+    return u2f(o);
 }
+static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 static inline double nan_io_d(double r, double io, double in) {
-    uint64_t u;
-    if (io != io) { memcpy(&u, &io, 8); u |= 0x8000000000000ull; memcpy(&r, &u, 8); return r; }
-    if (in != in) { memcpy(&u, &in, 8); u |= 0x8000000000000ull; memcpy(&r, &u, 8); return r; }
-    if (r != r) { u = 0xFFF8000000000000ull; memcpy(&r, &u, 8); }
-    return r;
+    uint64_t o = (r != r) ? 0xFFF8000000000000ull : d2u(r);
+    o = (in != in) ? (d2u(in) | 0x8000000000000ull) : o;
+    o = (io != io) ? (d2u(io) | 0x8000000000000ull) : o;
+    return u2d(o);
 }
 
 #define ORC_REDUCE_FP(T, NAN_IO)                                                       \
