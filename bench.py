@@ -174,7 +174,7 @@ def cpu_baseline(cfg, seconds):
                   f"GiB/s); 1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
         "port_1thread": port_1,
         "port_note": "port_1thread = oracle/comp_oracle.c on one thread, the restatement the parity tests use "
-                     "(it states the NaN rule per element, unvectorized: a checker, not the baseline)"
+                     "(it states the x86 NaN rule explicitly: a checker, not the baseline)"
         if port_1 is not None else None,
         "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": nt, "reps": rn,
                          "note": "range split over threads, emulating CCL_WORKER_COUNT"},
