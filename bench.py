@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's work")
     p.add_argument("--no-host-leg", action="store_true", help="skip the host-resident (PCIe) measurement")
+    p.add_argument("--no-config-legs", action="store_true",
+                   help="skip the other BASELINE configs' legs (timed launches + full parity) of a c2 run")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
                         "one GPU when rehearsing the N>1 path)")
@@ -343,6 +345,72 @@ def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, w
             "scaling": "strong", "note": "one bucket split by element range over the ranks, no collective"}
 
 
+def config_legs(m, stream, launches=10):
+    """The other BASELINE.json configs, each at its full size on this GPU, in
+    the same run as the headline: mean launch time of `launches` back-to-back
+    launches under one event pair, and the whole result checked bit for bit
+    (full_parity).  C1 (configs[0]) is the 512 KiB nreduce chunk of a 2-rank
+    1 MiB allreduce through ccl_comp_reduce on host buffers: the dispatcher
+    keeps it on the calling thread's CPU, as oneCCL runs it."""
+    import numpy as np
+    import torch
+
+    from oneccl_amd import _lib
+    legs = {}
+    sh = stream.cuda_stream
+    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod"):
+        desc, dt, es, op, k, bucket, flags = CONFIGS[name]
+        n = bucket // es
+        ins = [torch.empty(n, dtype=torch_dtype(dt), device="cuda") for _ in range(k)]
+        for j, t in enumerate(ins):
+            fill(t, 0xC0 + 131 * j)
+        arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
+
+        def step():
+            if k == 2:
+                return m.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)
+            return m.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
+
+        for _ in range(2):
+            _lib.check(step(), name)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(launches):
+            _lib.check(step(), name)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / launches
+        algo = (k + 1) * n * es
+        par = full_parity(lambda: _lib.check(step(), name), ins, k, dt, op, flags, 0xE0, "mi_reduce" if k == 2 else
+                          "mi_reduce_multi")
+        legs[name] = {"workload": desc, "GiBps": round(bucket / GiB / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
+                      "roofline_frac": round(algo / (ms / 1e3) / (HBM_PEAK_GBPS * 1e9), 4),
+                      "parity": {"elements": par["elements"], "mismatches": par["mismatches"]}}
+        del ins, arr
+        torch.cuda.empty_cache()
+    # C1: host buffers through the drop-in entry point
+    n = 131072
+    rng = np.random.default_rng(0xC1)
+    a = (rng.random(n, dtype=np.float32) * 2 - 1)
+    b0 = (rng.random(n, dtype=np.float32) * 2 - 1)
+    shim = _lib.shim()
+    b = b0.copy()
+    tt = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0), "ccl_comp_reduce")
+        tt.append(time.perf_counter() - t0)
+    b = b0.copy()
+    _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0), "ccl_comp_reduce")
+    exp = b0 + a  # IEEE RNE fp32 add, no NaNs in these inputs
+    legs["c1"] = {"workload": "512 KiB fp32 sum chunk (nreduce of a 2-rank 1 MiB allreduce), host buffers through "
+                              "ccl_comp_reduce (the dispatcher keeps it on the calling thread's CPU)",
+                  "median_us": round(statistics.median(tt) * 1e6, 2), "best_us": round(min(tt) * 1e6, 2),
+                  "parity": {"elements": n, "mismatches": int(np.count_nonzero(b.view(np.uint32) != exp.view(np.uint32)))}}
+    return legs
+
+
 def max_over_ranks(vals, world, device):
     """Max of each value over all ranks (the driver's contract: the slowest
     rank's time is the job's time)."""
@@ -545,6 +613,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, args.cpu_seconds)
 
+    legs = None
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_config_legs:
+        legs = config_legs(m, stream)
+
     # BASELINE configs[3] as written at N > 1: one 1 GiB bucket split over the
     # GPUs, beside the weak-scaling `value` (each GPU its own 1 GiB bucket):
     # the 2-input headline bucket and the 8-input fan-in
@@ -602,10 +674,13 @@ def main():
             out["dropin_sync"] = dropin
         if host_leg:
             out["host_resident"] = host_leg
+        if legs:
+            out["configs"] = legs
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
     bad = parity["mismatches"] + (dropin["parity"]["mismatches"] if dropin else 0)
+    bad += sum(v["parity"]["mismatches"] for v in (legs or {}).values())
     if bad:
         log(f"PARITY FAILURE: {bad} element(s) differ from the expected result")
         sys.exit(3)

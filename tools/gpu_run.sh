@@ -146,7 +146,7 @@ for step in "$@"; do
             pc=${PROF_CONFIG:-c2}; pd=prof; [ "$pc" = c2 ] || pd=prof_$pc
             (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$GRAFT_REPO_ROOT/$OUT/$pd" -o bench -- \
-                python3 "$GRAFT_REPO_ROOT/bench.py" --config "$pc" --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg \
+                python3 "$GRAFT_REPO_ROOT/bench.py" --config "$pc" --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg --no-config-legs \
                 > "$GRAFT_REPO_ROOT/$OUT/$pd.out" 2> "$GRAFT_REPO_ROOT/$OUT/$pd.err")
             rc=$?; echo "=== $pd rc=$rc" | tee -a "$OUT/steps.log"
             [ $rc -eq 0 ] || exit $rc ;;
@@ -163,7 +163,7 @@ for step in "$@"; do
                 (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv \
                     -d "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr" -o bench -- \
                     python3 "$GRAFT_REPO_ROOT/bench.py" --config "$pc" --steps 5 --warmup 2 --no-cpu-baseline \
-                    --no-host-leg > "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.err")
+                    --no-host-leg --no-config-legs > "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.out" 2> "$GRAFT_REPO_ROOT/$pdir/pmc_$ctr.err")
                 rc=$?; echo "=== pmc $pc $ctr rc=$rc" | tee -a "$OUT/steps.log"
                 [ $rc -eq 0 ] || exit $rc
             done ;;
