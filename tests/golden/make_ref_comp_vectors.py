@@ -17,6 +17,11 @@ Cases:
   batch    ccl_comp_batch_reduce, storage-precision chain (comp.cpp:236-245):
            5 inputs at unaligned offsets of one buffer, int32/int64/float32/
            float64 x four ops
+  keep     ccl_comp_batch_reduce's keep-precision mode (comp.cpp:214-234) for
+           the avx512f and avx512bf impls x four ops, composed from the
+           reference's compiled parts (the function itself reads
+           global_data::get()): its AVX-512 array-conversion bodies
+           (oracle/_ref/libref_comp.so) and CCL_REDUCE(float)
 Inputs: the cross product of 16 special values per type first (integers:
 0, +-1, extremes, values whose sums and products wrap; floating point: +-0,
 +-1, +-inf, quiet NaNs with payloads of both signs, a signalling NaN,
@@ -124,6 +129,41 @@ def _lib():
     return L
 
 
+REF_AVX_SO = ROOT / "oracle" / "_ref" / "libref_comp.so"
+
+
+def _lib_avx():
+    A = ctypes.CDLL(str(REF_AVX_SO))
+    A.ref_fp32_to_bf16.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    A.ref_bf16_to_fp32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    return A
+
+
+def _bf16_to_f32_arrays(A, src: np.ndarray) -> np.ndarray:
+    """ccl_convert_bf16_to_fp32_arrays for a non-scalar impl (bf16.cpp:152-169):
+    16-element loads, the reference's own body, then the scalar tail (<< 16)."""
+    src = np.ascontiguousarray(src)
+    out = np.empty(src.size, np.float32)
+    lim = src.size // 16 * 16
+    if lim:
+        assert A.ref_bf16_to_fp32(src.ctypes.data, out.ctypes.data, lim) == 0
+    out.view(np.uint32)[lim:] = src[lim:].astype(np.uint32) << 16
+    return out
+
+
+def _f32_to_bf16_arrays(A, src: np.ndarray, impl: int) -> np.ndarray:
+    """ccl_convert_fp32_to_bf16_arrays for a non-scalar impl (bf16.cpp:130-150):
+    16-element stores of the impl (avx512f truncation, avx512bf
+    VCVTNEPS2BF16), the reference's own bodies, then the scalar tail
+    (truncation)."""
+    out = np.empty(src.size, np.uint16)
+    lim = src.size // 16 * 16
+    if lim:
+        assert A.ref_fp32_to_bf16(impl, src.ctypes.data, out.ctypes.data, lim) == 0
+    out[lim:] = (src[lim:].view(np.uint32) >> 16).astype(np.uint16)
+    return out
+
+
 def batch_offsets(n: int) -> list[int]:
     """Element offsets of the K inputs in one buffer: gaps that leave every
     input at a different alignment (offsets[0] names inout, never read)."""
@@ -185,6 +225,30 @@ def generate() -> dict[str, np.ndarray]:
             arrs[key] = out
             cases.append({"key": key, "kind": "batch", "dtype": dt, "op": op, "count": N, "offsets": offs,
                           "out_count_written": oc.value != SENTINEL})
+    # keep-precision batch reduce (comp.cpp:214-234), composed from the
+    # reference's own compiled parts: its array conversions' 16-element
+    # AVX-512 bodies (libref_comp.so, bf16_intrisics.hpp:62-76) with the
+    # arrays' scalar tails (bf16.cpp:130-169), and CCL_REDUCE(float) on the fp32
+    # scratch (libref_ccl_comp.so).  The whole function calls
+    # global_data::get() for its float32 datatype, so it is not called itself.
+    A = _lib_avx()
+    for impl, iname in ((1, "avx512f"), (2, "avx512bf")):
+        rng = np.random.default_rng(0x4B + impl)
+        buf = np.concatenate([_pair(11, seed=0x4C + 16 * impl + j)[0] for j in range(K_BATCH + 1)])
+        buf = buf[:offs[-1] + N].copy()
+        inout = _pair(11, seed=0x4D + impl)[1]
+        arrs[f"kp_{impl}_buf"], arrs[f"kp_{impl}_inout"] = buf, inout
+        for op, oname in OPS.items():
+            acc = _bf16_to_f32_arrays(A, inout)
+            for o in offs[1:]:
+                tmp = _bf16_to_f32_arrays(A, buf[o:o + N])
+                assert L.ref_ccl_comp_reduce_regular(tmp.ctypes.data, N, acc.ctypes.data, None, 9, 4, op) == 0
+            out = _f32_to_bf16_arrays(A, acc, impl)
+            key = f"kp_{impl}_{oname}"
+            arrs[key] = out
+            cases.append({"key": key, "kind": "keep", "dtype": 11, "impl": impl, "op": op, "count": N,
+                          "offsets": offs})
+        del rng
     meta = {"generator": "tests/golden/make_ref_comp_vectors.py",
             "producer": "oracle/_ref/libref_ccl_comp.so = oracle/ref_comp_harness.cpp + reference src/comp/comp.cpp, "
                         "bf16/bf16.cpp, bf16/bf16_intrisics.cpp, fp16/fp16.cpp, fp16/fp16_intrisics.cpp, "

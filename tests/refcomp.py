@@ -34,6 +34,8 @@ def cases(kind: str):
             d["a"], d["b"] = arrs[f"reduce1_{c['dtype']}_in"], arrs[f"reduce1_{c['dtype']}_inout"]
         elif kind == "bf16s":
             d["a"], d["b"] = arrs["bf16s_in"], arrs["bf16s_inout"]
+        elif kind == "keep":
+            d["buf"], d["b"] = arrs[f"kp_{c['impl']}_buf"], arrs[f"kp_{c['impl']}_inout"]
         else:
             d["buf"], d["b"] = arrs[f"batch_{c['dtype']}_buf"], arrs[f"batch_{c['dtype']}_inout"]
         out.append(d)

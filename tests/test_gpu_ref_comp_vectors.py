@@ -152,3 +152,39 @@ def test_nan_rule_at_full_bucket_scale():
         _lib.check(m.mi_reduce(pa, pb, n, dt, 0, 0, _stream()))
         torch.cuda.synchronize()
         assert_same(from_dev(tb, b), exp, dt, f"dtype {dt} sparse NaN")
+
+
+def _keep_flags(impl):
+    return 0x4 | ((0x2 | 0x8) if impl == 2 else 0)
+
+
+@pytest.mark.parametrize("c", refcomp.cases("keep"), ids=lambda c: c["key"])
+def test_fused_keep_precision_matches_reference_parts(c):
+    """ccl_comp_batch_reduce's keep-precision mode (fp32 accumulate, one
+    rounding per impl, truncated count % 16 tail under avx512bf) as one fused
+    kernel, against the composition of the reference's own compiled parts."""
+    import torch
+    n = c["count"]
+    holders = [to_dev(c["b"])] + [to_dev(c["buf"][o:o + n].copy()) for o in c["offsets"][1:]]
+    to, po = to_dev(np.zeros_like(c["b"]))
+    arr = _lib.void_ptr_array([p for _, p in holders])
+    _lib.check(_lib.mi().mi_reduce_multi(arr, len(holders), po, n, 11, c["op"], _keep_flags(c["impl"]), _stream()))
+    torch.cuda.synchronize()
+    assert_same(from_dev(to, c["b"]), c["expected"], 11, c["key"])
+
+
+@pytest.mark.parametrize("c", refcomp.cases("keep"), ids=lambda c: c["key"])
+def test_dropin_keep_precision_on_device_matches_reference_parts(c, monkeypatch):
+    """The drop-in's ccl_comp_batch_reduce(bf16_keep_precision_mode = 1) on
+    device buffers with CCL_BF16 selecting the impl (env.cpp:711-713)."""
+    monkeypatch.setenv("CCL_BF16", {1: "avx512f", 2: "avx512bf"}[c["impl"]])
+    comp.env_reload()
+    try:
+        tbuf, pbuf = to_dev(c["buf"])
+        tb, pb = to_dev(c["b"])
+        comp.comp_batch_reduce(pbuf, c["offsets"], c["count"], pb, comp.datatype.bfloat16, comp.reduction(c["op"]),
+                               bf16_keep_precision_mode=1)
+        assert_same(from_dev(tb, c["b"]), c["expected"], 11, c["key"])
+    finally:
+        monkeypatch.delenv("CCL_BF16", raising=False)
+        comp.env_reload()

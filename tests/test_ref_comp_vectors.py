@@ -73,6 +73,20 @@ def test_oracle_batch_reduce_matches_reference_code(c):
     assert (oc is not None) == c["out_count_written"]
 
 
+def keep_flags(impl):
+    """The kernel / host-path flags of keep-precision batch reduce per bf16
+    impl (comp.cpp batch_reduce_body): fp32 accumulate, and for avx512bf RNE
+    with the truncated count % 16 tail."""
+    return 0x4 | ((0x2 | 0x8) if impl == 2 else 0)
+
+
+@pytest.mark.parametrize("c", refcomp.cases("keep"), ids=lambda c: c["key"])
+def test_oracle_keep_precision_matches_reference_parts(c):
+    b = c["b"].copy()
+    oracle.batch_reduce(c["buf"], c["offsets"], c["count"], b, 11, c["op"], 1, c["impl"])
+    _check(b, c["expected"], c["key"])
+
+
 def _host_supported():
     return _lib.shim().mi_host_supported() != 0
 
@@ -94,6 +108,17 @@ def test_dropin_host_path_matches_reference_code(c):
     flags = 0 if c["kind"] == "bf16s" else reference_flags(c["dtype"])
     _host_reduce([b, c["a"]], b, c["dtype"], c["op"], flags)  # acc = inout; acc = op(in, acc)
     _check(b, c["expected"], c["key"])
+
+
+@pytest.mark.parametrize("c", refcomp.cases("keep"), ids=lambda c: c["key"])
+def test_dropin_host_keep_precision_matches_reference_parts(c):
+    if not _host_supported():
+        pytest.skip("no AVX2/F16C")
+    n = c["count"]
+    ins = [c["b"].copy()] + [c["buf"][o:o + n].copy() for o in c["offsets"][1:]]
+    out = c["b"].copy()
+    _host_reduce(ins, out, 11, c["op"], keep_flags(c["impl"]))
+    _check(out, c["expected"], c["key"])
 
 
 @pytest.mark.parametrize("c", refcomp.cases("batch"), ids=lambda c: c["key"])
@@ -133,11 +158,13 @@ def test_dropin_host_acc32_nan_order(dt, flags, k, op):
 
 
 def test_fixture_covers_every_row():
-    got = {(c["kind"], c["dtype"], c["op"]) for k in ("reduce", "reduce1", "bf16s", "batch") for c in refcomp.cases(k)}
+    got = {(c["kind"], c["dtype"], c["op"]) for k in ("reduce", "reduce1", "bf16s", "batch", "keep")
+           for c in refcomp.cases(k)}
     want = {("reduce", dt, op) for dt in (0, 1, 2, 3, 4, 5, 6, 7, 9, 10) for op in range(4)}
     want |= {("reduce1", dt, op) for dt in (9, 10) for op in range(4)}
     want |= {("bf16s", 11, op) for op in range(4)}
     want |= {("batch", dt, op) for dt in (4, 6, 9, 10) for op in range(4)}
+    want |= {("keep", 11, op) for op in range(4)}
     assert got == want
     # both-NaN pairs are in every floating-point case (the unpinned payload rule of round 2)
     for c in refcomp.cases("reduce"):
@@ -221,3 +248,22 @@ def test_dropin_copy_matches_reference_copy(nontemporal):
                 _lib.check_shim(s.mi_ccl_comp_copy(src.ctypes.data + so, b.ctypes.data + do, nbytes, nontemporal),
                                 "ccl_comp_copy")
                 assert np.array_equal(a, b), (nbytes, so, do)
+
+
+@pytest.mark.parametrize("c", refcomp.cases("keep"), ids=lambda c: c["key"])
+def test_dropin_keep_precision_host_buffers_matches_reference_parts(c, monkeypatch):
+    """ccl_comp_batch_reduce(bf16_keep_precision_mode = 1) through the drop-in
+    on host buffers (the dispatcher's CPU path), CCL_BF16 selecting the impl."""
+    if not _host_supported():
+        pytest.skip("no AVX2/F16C")
+    from oneccl_amd import comp
+    monkeypatch.setenv("CCL_BF16", {1: "avx512f", 2: "avx512bf"}[c["impl"]])
+    comp.env_reload()
+    try:
+        buf, b = c["buf"].copy(), c["b"].copy()
+        comp.comp_batch_reduce(buf.ctypes.data, c["offsets"], c["count"], b.ctypes.data, comp.datatype.bfloat16,
+                               comp.reduction(c["op"]), bf16_keep_precision_mode=1)
+        _check(b, c["expected"], c["key"])
+    finally:
+        monkeypatch.delenv("CCL_BF16", raising=False)
+        comp.env_reload()
