@@ -188,3 +188,19 @@ def test_dropin_keep_precision_on_device_matches_reference_parts(c, monkeypatch)
     finally:
         monkeypatch.delenv("CCL_BF16", raising=False)
         comp.env_reload()
+
+
+@pytest.mark.parametrize("c", refcomp.cases("bf16s"), ids=lambda c: c["key"])
+def test_dropin_scalar_bf16_on_device_matches_reference(c, monkeypatch):
+    """ccl_comp_reduce on bf16 device buffers with CCL_BF16=scalar."""
+    monkeypatch.setenv("CCL_BF16", "scalar")
+    comp.env_reload()
+    try:
+        ta, pa = to_dev(c["a"])
+        tb, pb = to_dev(c["b"])
+        oc = comp.comp_reduce(pa, c["a"].size, pb, comp.datatype.bfloat16, comp.reduction(c["op"]))
+        assert oc == c["a"].size
+        assert_same(from_dev(tb, c["b"]), c["expected"], 11, c["key"])
+    finally:
+        monkeypatch.delenv("CCL_BF16", raising=False)
+        comp.env_reload()

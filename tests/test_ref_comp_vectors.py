@@ -267,3 +267,22 @@ def test_dropin_keep_precision_host_buffers_matches_reference_parts(c, monkeypat
     finally:
         monkeypatch.delenv("CCL_BF16", raising=False)
         comp.env_reload()
+
+
+@pytest.mark.parametrize("c", refcomp.cases("bf16s"), ids=lambda c: c["key"])
+def test_dropin_scalar_bf16_host_buffers_matches_reference(c, monkeypatch):
+    """ccl_comp_reduce on bf16 with CCL_BF16=scalar (ccl_bf16_reduce's scalar
+    branch, bf16.cpp:98-101) through the drop-in's CPU path."""
+    if not _host_supported():
+        pytest.skip("no AVX2/F16C")
+    from oneccl_amd import comp
+    monkeypatch.setenv("CCL_BF16", "scalar")
+    comp.env_reload()
+    try:
+        a, b = c["a"].copy(), c["b"].copy()
+        oc = comp.comp_reduce(a.ctypes.data, a.size, b.ctypes.data, comp.datatype.bfloat16, comp.reduction(c["op"]))
+        assert oc == a.size  # bf16.cpp:94-96 writes out_count
+        _check(b, c["expected"], c["key"])
+    finally:
+        monkeypatch.delenv("CCL_BF16", raising=False)
+        comp.env_reload()
