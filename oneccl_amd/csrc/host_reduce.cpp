@@ -251,6 +251,18 @@ void fold_fp(const void* const* inputs, int k, void* out, size_t count) {
     // Every group reads all its inputs before it stores, so `out` may alias
     // any input (the same elements of a later input are read first).
     size_t i = 0;
+    if (k == 2) {  // ccl_comp_reduce: four groups per iteration, loads first
+        const C* a = in[0];
+        const C* x = in[1];
+        for (; i + 4 * W <= count; i += 4 * W) {
+            const auto a0 = vload(a + i), a1 = vload(a + i + W), a2 = vload(a + i + 2 * W), a3 = vload(a + i + 3 * W);
+            const auto x0 = vload(x + i), x1 = vload(x + i + W), x2 = vload(x + i + 2 * W), x3 = vload(x + i + 3 * W);
+            vstore(o + i, vop_first<OP>(a0, x0));
+            vstore(o + i + W, vop_first<OP>(a1, x1));
+            vstore(o + i + 2 * W, vop_first<OP>(a2, x2));
+            vstore(o + i + 3 * W, vop_first<OP>(a3, x3));
+        }
+    }
     for (; i + W <= count; i += W) fp_group<C, OP>(in, k, i, o);
     if (i < count) {  // zero-padded last group
         const size_t r = count - i;
