@@ -796,17 +796,34 @@ def host_shard_probe(n, dt, es, op, flags):
                       "bucket_bytes": nn * es, "entry": "mi_reduce_multi_sync_sharded"}), flush=True)
 
 
-KERNEL_SOURCES = ("oneccl_amd/csrc/mi_reduce.hip", "oneccl_amd/csrc/reduce_kernels.hpp")
+KERNEL_LIB = "oneccl_amd/lib/libmi_reduce.so"
 
 
 def kernel_identity():
-    """sha256 (16 hex digits) of the kernel sources a PMC pass measured:
-    tools/pmc_traffic.py stores it with the pass, pmc_traffic() matches it."""
+    """sha256 (16 hex digits) of the device code a PMC pass measured: the
+    `.hip_fatbin` section of the built library (the gfx950 code object of
+    every kernel, block sizes included as template arguments), so host-side
+    edits to mi_reduce.hip leave a pass current and any kernel change does
+    not.  tools/pmc_traffic.py stores it with the pass, pmc_traffic() matches
+    it.  None when the library is not built."""
     import hashlib
-    h = hashlib.sha256()
-    for rel in KERNEL_SOURCES:
-        h.update((ROOT / rel).read_bytes())
-    return h.hexdigest()[:16]
+    import struct
+    try:
+        b = (ROOT / KERNEL_LIB).read_bytes()
+    except OSError:
+        return None
+    shoff, = struct.unpack_from("<Q", b, 0x28)  # ELF64 section header table
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+
+    def section(i):  # sh_name, sh_offset, sh_size
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", b, shoff + i * shentsize)
+        return name, off, size
+    stroff = section(shstrndx)[1]
+    for i in range(shnum):
+        name, off, size = section(i)
+        if b[stroff + name:b.index(b"\0", stroff + name)] == b".hip_fatbin":
+            return "fatbin:" + hashlib.sha256(b[off:off + size]).hexdigest()[:16]
+    return None
 
 
 def pmc_passes(config):
@@ -835,13 +852,13 @@ def pmc_traffic(config, algo_bytes):
     if not passes:
         return None
     ident = kernel_identity()
-    current = [pe for pe in passes if pe[1].get("kernel_sources") == ident]
+    current = [pe for pe in passes if ident and pe[1].get("kernel_code") == ident]
     pool = current or passes
     p, e = max(pool, key=lambda pe: (pe[1].get("recorded_utc", ""), str(pe[0])))
     pmc_algo = e["algorithmic_bytes_per_launch"]
     ratio = e["hbm_bytes_per_launch"] / pmc_algo
     src = str(p.relative_to(ROOT))
-    src += " (kernel sources match this tree)" if current else " (STALE: recorded against other kernel sources)"
+    src += " (device code matches this build)" if current else " (STALE: recorded against other device code)"
     if pmc_algo != algo_bytes:
         src += f" (ratio {ratio:.6f} of a {pmc_algo}-B launch, applied to this {algo_bytes}-B launch)"
     return {"bytes_per_launch": int(round(ratio * algo_bytes)), "ratio": round(ratio, 6), "source": src,

@@ -792,12 +792,19 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
         for (void* p : d->dbuf[s]) MI_HIP(hipFree(p));
         d->dbuf[s].clear();
     }
-    d->dbuf_bytes = std::max(bytes, d->dbuf_bytes);
+    const size_t want = std::max(bytes, d->dbuf_bytes);
     nbuf = std::max(nbuf, d->dbuf[0].size());
+    d->dbuf_bytes = 0;  // published only once every buffer exists: a failed
+                        // hipMalloc leaves no null slot behind for the next call
     for (int s = 0; s < 2; s++) {
-        d->dbuf[s].resize(nbuf, nullptr);
-        for (size_t i = 0; i < nbuf; i++) MI_HIP(hipMalloc(&d->dbuf[s][i], d->dbuf_bytes));
+        d->dbuf[s].reserve(nbuf);
+        while (d->dbuf[s].size() < nbuf) {
+            void* p = nullptr;
+            MI_HIP(hipMalloc(&p, want));
+            d->dbuf[s].push_back(p);
+        }
     }
+    d->dbuf_bytes = want;
     return 0;
 }
 

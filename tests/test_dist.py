@@ -132,3 +132,30 @@ def test_pmc_traffic_scales_to_the_launch():
     half = bench.pmc_traffic("c2", 3 * (1 << 29))
     assert abs(half["bytes_per_launch"] * 2 - full["bytes_per_launch"]) <= 2
     assert half["ratio"] == full["ratio"] and 0.99 < half["ratio"] < 1.01
+
+
+def test_kernel_identity_is_the_device_code():
+    """The PMC pass a bench line cites is matched by the hash of the built
+    library's device code (.hip_fatbin), not of source files: a host-only edit
+    keeps a pass current, a kernel change makes it stale."""
+    import hashlib
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    lib = os.path.join(root, bench.KERNEL_LIB)
+    objcopy = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
+    if not os.path.exists(lib) or not os.path.exists(objcopy):
+        pytest.skip("library or llvm-objcopy absent")
+    ident = bench.kernel_identity()
+    assert ident and ident.startswith("fatbin:")
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run([objcopy, f"--dump-section=.hip_fatbin={fat}", lib, os.path.join(d, "x.so")], check=True,
+                       capture_output=True)
+        with open(fat, "rb") as f:
+            assert ident == "fatbin:" + hashlib.sha256(f.read()).hexdigest()[:16]
+    passes = bench.pmc_passes("c2")
+    assert all("hbm_bytes_per_launch" in e for _, e in passes)
