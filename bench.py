@@ -844,8 +844,8 @@ def pmc_passes(config):
 def pmc_traffic(config, algo_bytes):
     """HBM bytes per launch from a committed rocprofv3 PMC pass (produced by
     tools/pmc_traffic.py).  The pass chosen is the one recorded against the
-    kernel sources of this tree (kernel_identity); failing that, the most
-    recently recorded one, marked stale.  The pass is a 1-GPU full-bucket
+    device code of this tree's build (kernel_identity); failing that, the
+    most recently recorded one, marked stale.  The pass is a 1-GPU full-bucket
     run; a launch of another size (a strong-scaling shard) gets the measured
     ratio to algorithmic bytes applied to its own algorithmic bytes."""
     passes = pmc_passes(config)

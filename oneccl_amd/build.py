@@ -126,6 +126,22 @@ def build_copy_sweep(force: bool = False) -> Path:
     return out
 
 
+def build_lds_stage_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "lds_stage_sweep"
+    src = ROOT / "tools" / "lds_stage_sweep.hip"
+    if src.exists() and (force or _stale(out, [src, CSRC / "reduce_kernels.hpp"])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
+def build_occupancy_sweep(force: bool = False) -> Path:
+    out = ROOT / "tools" / "occupancy_sweep"
+    src = ROOT / "tools" / "occupancy_sweep.hip"
+    if src.exists() and (force or _stale(out, [src, CSRC / "reduce_kernels.hpp"])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wall", "-o", str(out), str(src)])
+    return out
+
+
 def build_latency(force: bool = False) -> Path:
     out = ROOT / "tools" / "latency"
     src = ROOT / "tools" / "latency.hip"
@@ -220,6 +236,8 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_fan_sweep()
     build_burst_sweep()
     build_copy_sweep()
+    build_lds_stage_sweep()
+    build_occupancy_sweep()
     build_latency()
     build_segv_trace()
     if asan:

@@ -153,18 +153,39 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
 // kernel table
 // ---------------------------------------------------------------------------
 typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
+typedef hipError_t (*LaunchFanFn)(hipStream_t, const KArgs&, unsigned lds);
 typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
 typedef hipError_t (*LaunchBFn)(dim3, hipStream_t, const BArgs&);
 
 // Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
 constexpr int kB2 = 1024;
 constexpr int kU2 = 1;
-// Buffer-addressed fan-in, one tile per block (profiles/round1_sweep7_fan_buffer*.jsonl),
-// 1024-lane tiles for every type: 8- and 16-bit integers fold packed on dwords
+// Buffer-addressed fan-in, one tile per block.  One-wave (64-lane) tiles,
+// with the waves resident on a CU capped by LDS that no instruction touches
+// (a block that reserves 1/W of a CU's LDS leaves room for W of them).  Each
+// wave holds K one-KiB loads in flight, and the fan-in streams fastest with
+// ~50-100 KiB of loads in flight per CU: at the library's former 1024-lane
+// tiles and 32 waves per CU, 8 inputs kept 256 KiB per CU in flight and ran
+// 10-11 % slower (tools/occupancy_sweep.hip, profiles/round3_occupancy/:
+// 8 inputs 1.65 -> 1.47 ms per GiB, 6 inputs -10.7 %, 4 inputs -4.7 %,
+// 16 inputs -7.4 %).  8- and 16-bit integers fold packed on dwords
 // (pk_op4), so no type unpacks more than 8 elements per vector.
-template <typename Tag>
-constexpr int fan_block() {
-    return 1024;
+constexpr int kFanBlock = 64;
+int fan_waves_per_cu(int k) { return k <= 4 ? 16 : k <= 6 ? 12 : k <= 8 ? 10 : k <= 12 ? 8 : 6; }
+
+// LDS bytes per CU of each device (read once per device; 0 = unknown: no cap)
+unsigned lds_per_cu(int device) {
+    static std::mutex mu;
+    static std::vector<int> cache;  // -1: not read yet
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0) return 0;
+    if ((size_t)device >= cache.size()) cache.resize(device + 1, -1);
+    if (cache[device] < 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess) v = 0;
+        cache[device] = std::max(v, 0);
+    }
+    return (unsigned)cache[device];
 }
 
 template <typename Tag, int OP, unsigned V>
@@ -186,14 +207,14 @@ hipError_t launch_batch(dim3 grid, hipStream_t s, const BArgs& a) {
 }
 
 template <typename Tag, int OP, unsigned V>
-hipError_t launch_fan(dim3, hipStream_t s, const KArgs& a) {
-    constexpr int B = fan_block<Tag>();
+hipError_t launch_fan(hipStream_t s, const KArgs& a, unsigned lds) {
+    constexpr int B = kFanBlock;
     const uint64_t blocks = std::max<uint64_t>((a.nvec + B - 1) / B, 1);
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
     if (a.k <= 8)
-        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, 8>), dim3((unsigned)blocks), dim3(B), 0, s, a);
+        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, 8>), dim3((unsigned)blocks), dim3(B), lds, s, a);
     else
-        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, kMaxInputs>), dim3((unsigned)blocks), dim3(B), 0, s, a);
+        hipLaunchKernelGGL((fan_kernel<Tag, OP, V, B, kMaxInputs>), dim3((unsigned)blocks), dim3(B), lds, s, a);
     return hipGetLastError();
 }
 
@@ -203,7 +224,7 @@ hipError_t launch_fan(dim3, hipStream_t s, const KArgs& a) {
 struct Kern {
     LaunchFn general = nullptr;
     Launch2Fn lean = nullptr;
-    LaunchFn fan = nullptr;
+    LaunchFanFn fan = nullptr;
     LaunchBFn batch = nullptr;
 };
 
@@ -389,9 +410,12 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         } else {
             a.scalar_only = 1;
         }
-        // fan tiles are >= 256 vectors: one launch covers 2^39 vectors
-        if (vec && cap == 0 && nvec / 256 < 0x7FFFFFFFull) {
-            e = kern.fan(dim3(0), stream, a);
+        // fan tiles are 64 vectors: one launch covers 2^37 vectors (2 TiB)
+        if (vec && cap == 0 && nvec / kFanBlock < 0x7FFFFFFFull) {
+            int dev = -1;  // the device the stream launches on
+            if (!stream || hipStreamGetDevice(stream, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+            const unsigned lds = lds_per_cu(dev) / (unsigned)fan_waves_per_cu(k);
+            e = kern.fan(stream, a, lds);
         } else {
             uint64_t blocks;
             if (vec) {

@@ -397,9 +397,9 @@ def test_grid_stride_general_kernel(dt, op, k):
 
 
 def test_fanin_beyond_32_bit_indices():
-    """3-input int8 fan-in past 2^32 elements: 1024-lane fan tiles of 16-byte
-    vectors (16 KiB = 2^14 elements per block, folded packed on dwords), so
-    2^18 + 1 blocks."""
+    """3-input int8 fan-in past 2^32 elements: 64-lane fan tiles of 16-byte
+    vectors (1 KiB = 2^10 elements per block, folded packed on dwords), so
+    2^22 + 1 blocks."""
     import torch
     n = (1 << 32) + 4099
     rng = np.random.default_rng(11)

@@ -57,6 +57,15 @@ for step in "$@"; do
             python tools/pmc_burst.py "$OUT/pmc_burst.json" "$OUT/pmcburst" > "$OUT/pmc_burst.out" 2>&1 ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
+        ldsstage)  # inputs staged through LDS by LDS-DMA vs the library's register path (C2, C3, C4)
+            run ldsstage 300 ./tools/lds_stage_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
+        occ)  # block size x resident-wave cap (idle LDS) for the C2 / C3 / C4 kernels
+            run occ 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 ${OCC_WHICH:-all} &&
+            run occ_bf 300 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 c4bf ;;
+        occr2)  # the 2-input kernel in place: block size and wave cap, per dtype
+            run occr2 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 r2ab ;;
+        occk)  # the 64-lane fan-in over input count x wave cap
+            run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)
             run copysweep 300 ./tools/copy_sweep 1024 ${SWEEP_ROUNDS:-4} 8 ;;
         copyprof)  # per-kernel durations of every copy_sweep variant

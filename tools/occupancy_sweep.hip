@@ -1,0 +1,363 @@
+// occupancy_sweep.hip — experiment: block size and resident waves per CU for
+// the library's streaming kernels.
+//
+// tools/lds_stage_sweep.hip found the 8-input fan-in 2.6 % faster at 128-lane
+// blocks than at the library's 1024, and 4.3 % faster again when each block
+// also held 16 KiB of idle LDS (10 blocks = 20 waves per CU instead of 32),
+// while staging the inputs through LDS itself gained nothing.  Here every
+// (kernel, block size, resident-wave cap) is timed in interleaved rounds.
+// The cap is set the way a kernel without LDS traffic can set it: dynamic
+// LDS that no instruction touches, sized so floor(160 KiB / bytes) blocks fit
+// on a CU; hipOccupancyMaxActiveBlocksPerMultiprocessor reports what the
+// runtime actually grants.  Outputs are checked bit for bit against the
+// library's default launch before timing.
+//
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab]   (all = c2, c3, c4)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <type_traits>
+#include <string>
+#include <vector>
+
+#include "../oneccl_amd/csrc/reduce_kernels.hpp"
+
+using namespace mi;
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e = (x);                                                              \
+        if (e != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+constexpr unsigned kLdsPerCU = 160 * 1024;
+
+__global__ void fill_kernel(uint32_t* p, uint64_t nwords, uint32_t seed, uint32_t mask, uint32_t bits) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
+        h ^= h >> 15;
+        h *= 0x2C1B3C6Du;
+        h ^= h >> 12;
+        p[i] = (h & mask) | bits;
+    }
+}
+
+__global__ void count_diff(const uint32_t* a, const uint32_t* b, uint64_t nwords, unsigned long long* bad) {
+    unsigned long long n = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * blockDim.x)
+        n += a[i] != b[i];
+    if (n) atomicAdd(bad, n);
+}
+
+struct Variant {
+    std::string name;
+    std::string group;
+    double traffic;
+    std::function<hipError_t(hipStream_t)> run;
+    void* out;
+    void* ref;  // nullptr: the group's reference launch
+    size_t bytes;
+    std::vector<float> ms;
+};
+
+// dynamic LDS that leaves room for `blocks` blocks per CU (0: none)
+unsigned lds_for(int blocks) { return blocks > 0 ? kLdsPerCU / blocks : 0; }
+
+// one variant per (group, kernel, block size, LDS bytes): caps that round to
+// the same blocks per CU are timed once
+bool seen(const std::string& key) {
+    static std::vector<std::string> keys;
+    if (std::find(keys.begin(), keys.end(), key) != keys.end()) return true;
+    keys.push_back(key);
+    return false;
+}
+
+template <typename F>
+int granted(F kernel, int B, unsigned lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, B, lds) != hipSuccess) return -1;
+    return nb;
+}
+
+template <typename Tag, unsigned V, int B>
+void add_r2(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes, int cap_waves, void* ref) {
+    const unsigned blocks = (unsigned)(r.nvec / B);
+    const int waves = B / 64;
+    const unsigned lds = cap_waves ? lds_for(cap_waves / waves) : 0;
+    if ((cap_waves && cap_waves < waves) || seen(std::string(group) + "r2/" + std::to_string(B) + "/" +
+                                                 std::to_string(lds) + (ref ? "" : "/ref")))
+        return;
+    auto k = reduce2_kernel<Tag, OP_SUM, V, 1, B>;
+    const int nb = granted(k, B, lds);
+    char name[200];
+    snprintf(name, sizeof name, "%s reduce2_kernel %dx1, lds %u B/block -> %d blocks = %d waves per CU", group, B, lds,
+             nb, nb * waves);
+    vs.push_back({name, group, 3.0 * bytes, [r, blocks, lds](hipStream_t s) {
+                      hipLaunchKernelGGL((reduce2_kernel<Tag, OP_SUM, V, 1, B>), dim3(blocks), dim3(B), lds, s, r);
+                      return hipGetLastError();
+                  }, r.out, ref, bytes, {}});
+}
+
+template <typename Tag, unsigned V, int B, int KMAX = 8>
+void add_fan(std::vector<Variant>& vs, const char* group, KArgs a, size_t bytes, int cap_waves, void* ref) {
+    const unsigned blocks = (unsigned)(a.nvec / B);
+    const int waves = B / 64;
+    const unsigned lds = cap_waves ? lds_for(cap_waves / waves) : 0;
+    if ((cap_waves && cap_waves < waves) || seen(std::string(group) + "fan/" + std::to_string(B) + "/" +
+                                                 std::to_string(lds) + (ref ? "" : "/ref")))
+        return;
+    auto k = fan_kernel<Tag, OP_SUM, V, B, KMAX>;
+    const int nb = granted(k, B, lds);
+    char name[200];
+    snprintf(name, sizeof name, "%s fan_kernel %dx1, lds %u B/block -> %d blocks = %d waves per CU", group, B, lds, nb,
+             nb * waves);
+    vs.push_back({name, group, (a.k + 1.0) * bytes, [a, blocks, lds](hipStream_t s) {
+                      hipLaunchKernelGGL((fan_kernel<Tag, OP_SUM, V, B, KMAX>), dim3(blocks), dim3(B), lds, s, a);
+                      return hipGetLastError();
+                  }, a.out, ref, bytes, {}});
+}
+
+// every block size at every cap (caps a block size cannot meet are skipped)
+constexpr int kCaps[] = {0, 24, 20, 16, 12, 8, 6, 4};
+
+template <typename Tag, unsigned V>
+void sweep_r2(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes, void* out_alt) {
+    add_r2<Tag, V, 1024>(vs, group, r, bytes, 0, nullptr);  // the library's launch: the reference
+    void* ref = r.out;
+    r.out = out_alt;
+    for (int cap : kCaps) {
+        add_r2<Tag, V, 1024>(vs, group, r, bytes, cap, ref);
+        add_r2<Tag, V, 512>(vs, group, r, bytes, cap, ref);
+        add_r2<Tag, V, 256>(vs, group, r, bytes, cap, ref);
+        add_r2<Tag, V, 128>(vs, group, r, bytes, cap, ref);
+        add_r2<Tag, V, 64>(vs, group, r, bytes, cap, ref);
+    }
+}
+
+template <typename Tag, unsigned V>
+void sweep_fan(std::vector<Variant>& vs, const char* group, KArgs a, size_t bytes, void* out_alt) {
+    add_fan<Tag, V, 1024>(vs, group, a, bytes, 0, nullptr);
+    void* ref = a.out;
+    a.out = out_alt;
+    for (int cap : kCaps) {
+        add_fan<Tag, V, 1024>(vs, group, a, bytes, cap, ref);
+        add_fan<Tag, V, 128>(vs, group, a, bytes, cap, ref);
+        add_fan<Tag, V, 64>(vs, group, a, bytes, cap, ref);
+    }
+}
+
+int main(int argc, char** argv) {
+    const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1024;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 6;
+    const int reps = argc > 3 ? atoi(argv[3]) : 8;
+    const std::string which = argc > 4 ? argv[4] : "all";
+    const size_t bytes = mib << 20, bytes3 = bytes / 4;
+    if (bytes3 % (64 * 1024) != 0) {
+        fprintf(stderr, "bucket must be a multiple of 256 MiB\n");
+        return 2;
+    }
+    std::vector<void*> buf(10);
+    for (auto& p : buf) CK(hipMalloc(&p, bytes));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    for (int i = 0; i < 8; i++)
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)buf[i], bytes / 4, 0xA0u + i,
+                           0x007FFFFFu, 0x3F800000u);
+    CK(hipStreamSynchronize(s));
+
+    std::vector<Variant> vs;
+    if (which == "all" || which == "c2") {
+        R2Args r{};
+        r.acc = buf[0];
+        r.in = buf[1];
+        r.out = buf[8];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        sweep_r2<float, 0u>(vs, "C2 fp32 sum 1 GiB:", r, bytes, buf[9]);
+    }
+    if (which == "all" || which == "c3") {
+        // bf16 operands in buffers of their own
+        void *la, *lb;
+        CK(hipMalloc(&la, bytes3));
+        CK(hipMalloc(&lb, bytes3));
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)la, bytes3 / 4, 0x1234u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)lb, bytes3 / 4, 0x4321u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        R2Args r{};
+        r.acc = la;
+        r.in = lb;
+        r.out = static_cast<char*>(buf[8]) + bytes / 2;
+        r.nvec = bytes3 / 16;
+        r.trunc_from = bytes3 / 2;
+        sweep_r2<bf16_tag, V_BF16_RNE>(vs, "C3 bf16 sum 256 MiB:", r, bytes3, static_cast<char*>(buf[9]) + bytes / 2);
+    }
+    if (which == "all" || which == "c4") {
+        KArgs a{};
+        for (int i = 0; i < 8; i++) a.in[i] = buf[i];
+        a.out = buf[8];
+        a.k = 8;
+        a.count = bytes / 4;
+        a.nvec = bytes / 16;
+        a.trunc_from = a.count;
+        sweep_fan<float, 0u>(vs, "C4 fp32 8-input 1 GiB:", a, bytes, buf[9]);
+        KArgs a4 = a;
+        a4.k = 4;
+        sweep_fan<float, 0u>(vs, "fan-in fp32 4-input 1 GiB:", a4, bytes, buf[9]);
+    }
+    if (which == "r2ab") {
+        // the 2-input kernel in place (out = the accumulator, as ccl_comp_reduce
+        // and the bench run it), a focused set of shapes, per dtype
+        void *la, *lb;
+        CK(hipMalloc(&la, bytes3));
+        CK(hipMalloc(&lb, bytes3));
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)la, bytes3 / 4, 0x1234u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)lb, bytes3 / 4, 0x4321u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        auto shapes = [&](auto tag, auto vconst, const char* g, R2Args r, size_t nbytes) {
+            using Tag = decltype(tag);
+            constexpr unsigned V = decltype(vconst)::value;
+            // in place, every variant rewrites the same accumulator: nothing to
+            // compare against (the out-of-place modes check the same kernels)
+            add_r2<Tag, V, 1024>(vs, g, r, nbytes, 0, nullptr);
+            add_r2<Tag, V, 512>(vs, g, r, nbytes, 0, nullptr);
+            add_r2<Tag, V, 256>(vs, g, r, nbytes, 0, nullptr);
+            add_r2<Tag, V, 128>(vs, g, r, nbytes, 0, nullptr);
+            add_r2<Tag, V, 64>(vs, g, r, nbytes, 0, nullptr);
+            add_r2<Tag, V, 128>(vs, g, r, nbytes, 24, nullptr);
+            add_r2<Tag, V, 64>(vs, g, r, nbytes, 24, nullptr);
+            add_r2<Tag, V, 64>(vs, g, r, nbytes, 20, nullptr);
+            add_r2<Tag, V, 64>(vs, g, r, nbytes, 16, nullptr);
+        };
+        R2Args r{};
+        r.acc = buf[0];
+        r.in = buf[1];
+        r.out = buf[0];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        shapes(float(), std::integral_constant<unsigned, 0u>(), "C2 fp32 sum 1 GiB in place:", r, bytes);
+        R2Args ri = r;
+        ri.acc = ri.out = buf[2];
+        ri.in = buf[3];
+        shapes(int32_t(), std::integral_constant<unsigned, 0u>(), "C5 int32 sum 1 GiB in place:", ri, bytes);
+        R2Args rb{};
+        rb.acc = rb.out = la;
+        rb.in = lb;
+        rb.nvec = bytes3 / 16;
+        rb.trunc_from = bytes3 / 2;
+        shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
+        shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "fank") {
+        // the fan-in at 64-lane blocks over the input count and the wave cap
+        // (16 inputs: 8 more buffers)
+        for (int i = 0; i < 8; i++) {
+            void* p;
+            CK(hipMalloc(&p, bytes));
+            hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)p, bytes / 4, 0xC0u + i, 0x007FFFFFu,
+                               0x3F800000u);
+            buf.push_back(p);
+        }
+        static std::vector<std::string> names;
+        for (int k : {3, 4, 6, 8, 12, 16}) {
+            KArgs a{};
+            for (int i = 0; i < k; i++) a.in[i] = buf[i < 8 ? i : i + 2];  // skip the two output buffers
+            a.out = buf[8];
+            a.k = k;
+            a.count = bytes / 4;
+            a.nvec = bytes / 16;
+            a.trunc_from = a.count;
+            names.push_back("fan-in fp32 " + std::to_string(k) + "-input 1 GiB:");
+            const char* g = names.back().c_str();
+            if (k <= 8) {
+                add_fan<float, 0u, 1024, 8>(vs, g, a, bytes, 0, nullptr);
+                KArgs b = a;
+                b.out = buf[9];
+                for (int cap : {0, 32, 24, 21, 16, 12, 10, 8, 6, 4}) add_fan<float, 0u, 64, 8>(vs, g, b, bytes, cap, a.out);
+            } else {
+                add_fan<float, 0u, 1024, 16>(vs, g, a, bytes, 0, nullptr);
+                KArgs b = a;
+                b.out = buf[9];
+                for (int cap : {0, 32, 24, 21, 16, 12, 10, 8, 6, 4}) add_fan<float, 0u, 64, 16>(vs, g, b, bytes, cap, a.out);
+            }
+        }
+    }
+    if (which == "c4bf") {
+        // bf16 inputs accumulated in fp32 (the bench's c4-bf16acc leg), in a
+        // run of its own: the inputs are refilled as bf16 pairs (fp32 bits
+        // read as bf16 would hold NaN patterns)
+        for (int i = 0; i < 8; i++)
+            hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)buf[i], bytes / 4, 0xB0u + i,
+                               0x3FFF3FFFu, 0x3C003C00u);
+        KArgs a{};
+        for (int i = 0; i < 8; i++) a.in[i] = buf[i];
+        a.out = buf[8];
+        a.k = 8;
+        a.count = bytes / 2;
+        a.nvec = bytes / 16;
+        a.trunc_from = a.count;
+        sweep_fan<bf16_tag, V_ACC_FP32 | V_BF16_RNE>(vs, "C4 bf16 8-input fp32-acc 1 GiB:", a, bytes, buf[9]);
+    }
+    CK(hipStreamSynchronize(s));
+
+    // check: each group's reference first (in order), then every variant against it;
+    // a variant whose launch fails (a cap the device cannot grant) is dropped
+    unsigned long long* bad;
+    CK(hipMalloc(&bad, sizeof(*bad)));
+    std::vector<Variant> ok;
+    for (auto& v : vs) {
+        if (v.run(s) != hipSuccess) {
+            fprintf(stderr, "skip (launch failed): %s\n", v.name.c_str());
+            continue;
+        }
+        if (v.ref) {
+            CK(hipMemsetAsync(bad, 0, sizeof(*bad), s));
+            hipLaunchKernelGGL(count_diff, dim3(4096), dim3(256), 0, s, (const uint32_t*)v.out, (const uint32_t*)v.ref,
+                               v.bytes / 4, bad);
+            unsigned long long h = 0;
+            CK(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            if (h) {
+                fprintf(stderr, "MISMATCH %llu words: %s\n", h, v.name.c_str());
+                return 3;
+            }
+        }
+        CK(hipStreamSynchronize(s));
+        ok.push_back(v);
+    }
+    fprintf(stderr, "%zu variants checked bit-exact against the library's launch\n", ok.size());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : ok)
+            for (int i = 0; i < reps; i++) {
+                CK(hipEventRecord(e0, s));
+                CK(v.run(s));
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        fprintf(stderr, "round %d/%d done\n", r + 1, rounds);
+    }
+    for (auto& v : ok) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2], best = v.ms.front();
+        printf("{\"variant\": \"%s\", \"bytes_per_launch\": %.0f, \"median_ms\": %.5f, \"best_ms\": %.5f, "
+               "\"median_TBps\": %.3f, \"best_TBps\": %.3f, \"frac_of_8TBps\": %.4f}\n",
+               v.name.c_str(), v.traffic, med, best, v.traffic / (med * 1e-3) / 1e12, v.traffic / (best * 1e-3) / 1e12,
+               v.traffic / (med * 1e-3) / 8e12);
+    }
+    for (auto& p : buf) CK(hipFree(p));
+    return 0;
+}
