@@ -154,12 +154,18 @@ unsigned canon_flags(int dt, int op, unsigned f, int k) {
 // ---------------------------------------------------------------------------
 typedef hipError_t (*LaunchFn)(dim3, hipStream_t, const KArgs&);
 typedef hipError_t (*LaunchFanFn)(hipStream_t, const KArgs&, unsigned lds);
-typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&);
-typedef hipError_t (*LaunchBFn)(dim3, hipStream_t, const BArgs&);
+typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&, unsigned lds);
+typedef hipError_t (*LaunchBFn)(dim3, hipStream_t, const BArgs&, unsigned lds);
 
-// Lean 2-input kernel shape (tools/reduce_sweep.hip, profiles/round1_sweep*.jsonl)
-constexpr int kB2 = 1024;
+// Lean 2-input kernel shape: one 16-byte vector per lane, one-wave (64-lane)
+// tiles, 24 waves resident per CU (capped by idle LDS, as the fan-in below).
+// In place, as ccl_comp_reduce runs it, that took 0.484 ms per GiB of fp32
+// against 0.508 for round 2's 1024-lane tiles at 32 waves per CU (-4.8 %;
+// int32 -3.5 %, bf16 -4.1 %, fp16 -3.5 %; tools/occupancy_sweep.hip r2ab,
+// profiles/round3_occupancy/).  Round 1's sweeps had stopped at 256 lanes.
+constexpr int kB2 = 64;
 constexpr int kU2 = 1;
+constexpr int kLeanWavesPerCU = 24;
 // Buffer-addressed fan-in, one tile per block.  One-wave (64-lane) tiles,
 // with the waves resident on a CU capped by LDS that no instruction touches
 // (a block that reserves 1/W of a CU's LDS leaves room for W of them).  Each
@@ -188,6 +194,14 @@ unsigned lds_per_cu(int device) {
     return (unsigned)cache[device];
 }
 
+// Dynamic LDS (never touched) for a one-wave block so that `waves` of them
+// fit on a CU of the device `s` launches on.
+unsigned wave_cap_lds(hipStream_t s, int waves) {
+    int dev = -1;
+    if (!s || hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    return lds_per_cu(dev) / (unsigned)waves;
+}
+
 template <typename Tag, int OP, unsigned V>
 hipError_t launch_general(dim3 grid, hipStream_t s, const KArgs& a) {
     hipLaunchKernelGGL((reduce_kernel<Tag, OP, V, 0, kUnroll, kMem>), grid, dim3(kBlock), 0, s, a);
@@ -195,14 +209,14 @@ hipError_t launch_general(dim3 grid, hipStream_t s, const KArgs& a) {
 }
 
 template <typename Tag, int OP, unsigned V>
-hipError_t launch_lean(dim3 grid, hipStream_t s, const R2Args& a) {
-    hipLaunchKernelGGL((reduce2_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), 0, s, a);
+hipError_t launch_lean(dim3 grid, hipStream_t s, const R2Args& a, unsigned lds) {
+    hipLaunchKernelGGL((reduce2_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), lds, s, a);
     return hipGetLastError();
 }
 
 template <typename Tag, int OP, unsigned V>
-hipError_t launch_batch(dim3 grid, hipStream_t s, const BArgs& a) {
-    hipLaunchKernelGGL((reduce2_batch_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), 0, s, a);
+hipError_t launch_batch(dim3 grid, hipStream_t s, const BArgs& a, unsigned lds) {
+    hipLaunchKernelGGL((reduce2_batch_kernel<Tag, OP, V, kU2, kB2>), grid, dim3(kB2), lds, s, a);
     return hipGetLastError();
 }
 
@@ -394,7 +408,7 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         const uint64_t tile = (uint64_t)kB2 * kU2;
         uint64_t blocks = std::max<uint64_t>((nvec + tile - 1) / tile, 1);
         if (blocks > 0x7FFFFFFFull) return fail(MI_E_UNSUPPORTED, "bucket too large for one launch");
-        e = kern.lean(dim3((unsigned)blocks), stream, r);
+        e = kern.lean(dim3((unsigned)blocks), stream, r, wave_cap_lds(stream, kLeanWavesPerCU));
     } else {
         KArgs a;
         memset(&a, 0, sizeof(a));
@@ -412,10 +426,7 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         }
         // fan tiles are 64 vectors: one launch covers 2^37 vectors (2 TiB)
         if (vec && cap == 0 && nvec / kFanBlock < 0x7FFFFFFFull) {
-            int dev = -1;  // the device the stream launches on
-            if (!stream || hipStreamGetDevice(stream, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-            const unsigned lds = lds_per_cu(dev) / (unsigned)fan_waves_per_cu(k);
-            e = kern.fan(stream, a, lds);
+            e = kern.fan(stream, a, wave_cap_lds(stream, fan_waves_per_cu(k)));
         } else {
             uint64_t blocks;
             if (vec) {
@@ -502,7 +513,7 @@ int launch_reduce_batch(const mi_reduce_desc_t* d, int n, int dt, int op, unsign
     auto flush = [&]() -> int {
         if (!a.n) return 0;
         a.block0[a.n] = (uint32_t)blocks;
-        const hipError_t e = kern.batch(dim3((unsigned)blocks), stream, a);
+        const hipError_t e = kern.batch(dim3((unsigned)blocks), stream, a, wave_cap_lds(stream, kLeanWavesPerCU));
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
         memset(&a, 0, sizeof(a));
         blocks = 0;
