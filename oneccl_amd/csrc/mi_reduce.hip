@@ -1281,11 +1281,17 @@ bool needs_staging(const void* const* inputs, int k, const void* out) {
 // ---------------------------------------------------------------------------
 // conversions
 // ---------------------------------------------------------------------------
-typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&);
+typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&, unsigned lds);
+
+// One-wave blocks, 24 resident per CU, as the 2-input reduce: 2^28 fp32 ->
+// bf16 0.253 -> 0.243 ms, bf16 -> fp32 0.262 -> 0.239 ms against round 2's
+// 256-lane blocks (tools/occupancy_sweep.hip copyconv, profiles/round3_occupancy/).
+constexpr int kConvBlock = 64;
+constexpr int kConvWavesPerCU = 24;
 
 template <typename ST, typename DT, unsigned V>
-hipError_t conv_one(dim3 grid, hipStream_t s, const CArgs& a) {
-    hipLaunchKernelGGL((convert_kernel<ST, DT, V>), grid, dim3(kBlock), 0, s, a);
+hipError_t conv_one(dim3 grid, hipStream_t s, const CArgs& a, unsigned lds) {
+    hipLaunchKernelGGL((convert_kernel<ST, DT, V, kConvBlock>), grid, dim3(kConvBlock), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1325,11 +1331,11 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     a.head = vec ? std::min<uint64_t>(((16 - (da & 15u)) & 15u) / ds, count) : 0;
     a.ngroups = vec ? (count - a.head) / 8 : 0;
     const uint64_t work = a.scalar_only ? count : std::max<uint64_t>(a.ngroups, 1);
-    uint64_t blocks = std::min<uint64_t>((work + kBlock - 1) / kBlock, 1u << 20);
+    uint64_t blocks = std::min<uint64_t>((work + kConvBlock - 1) / kConvBlock, 1u << 20);
     const int cap = max_blocks();  // a grid cap (mi_set_max_blocks) makes the kernel stride
     if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
     blocks = std::max<uint64_t>(blocks, 1);
-    hipError_t e = fn(dim3((unsigned)blocks), s, a);
+    hipError_t e = fn(dim3((unsigned)blocks), s, a, wave_cap_lds(s, kConvWavesPerCU));
     if (e != hipSuccess) return hip_fail(e, "convert kernel launch");
     return 0;
 }

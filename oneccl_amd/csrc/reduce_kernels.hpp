@@ -1104,9 +1104,9 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(const char* __restrict__ s
 // median with nt loads and stores against 5.78 for copy_kernel<2>).
 // copy_kernel stays for a capped grid (mi_set_max_blocks).
 constexpr int kCopyBlock = 512;
-template <int MEM>
-__global__ __launch_bounds__(kCopyBlock) void copy_lean_kernel(const char* __restrict__ src8, char* __restrict__ dst8,
-                                                               uint32_t head, uint64_t nvec, uint32_t tail) {
+template <int MEM, int B = kCopyBlock>
+__global__ __launch_bounds__(B) void copy_lean_kernel(const char* __restrict__ src8, char* __restrict__ dst8,
+                                                      uint32_t head, uint64_t nvec, uint32_t tail) {
     if (blockIdx.x == 0) {
         if (threadIdx.x < head) dst8[threadIdx.x] = src8[threadIdx.x];
         if (threadIdx.x < tail) {
@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(kCopyBlock) void copy_lean_kernel(const char* __res
             dst8[o] = src8[o];
         }
     }
-    const uint64_t v = (uint64_t)blockIdx.x * kCopyBlock + threadIdx.x;
+    const uint64_t v = (uint64_t)blockIdx.x * B + threadIdx.x;
     if (v < nvec)
         vstore<MEM & 2>(reinterpret_cast<u32x4*>(dst8 + head) + v,
                         vload<MEM & 1>(reinterpret_cast<const u32x4*>(src8 + head) + v));

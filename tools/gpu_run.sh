@@ -64,6 +64,8 @@ for step in "$@"; do
             run occ_bf 300 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 c4bf ;;
         occr2)  # the 2-input kernel in place: block size and wave cap, per dtype
             run occr2 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 r2ab ;;
+        occcopy)  # the copy and conversion kernels: block size and wave cap
+            run occcopy 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 copyconv ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)

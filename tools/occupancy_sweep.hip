@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -255,6 +255,71 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "copyconv") {
+        // ccl_comp_copy's device kernel (1 GiB, nt loads and stores) and the
+        // array conversions (2^28 elements): the library's block vs one-wave
+        // blocks under wave caps
+        const uint64_t nvec = bytes / 16;
+        auto add_copy = [&](auto bconst, int cap, void* ref) {
+            constexpr int B = decltype(bconst)::value;
+            const unsigned lds = cap ? lds_for(cap / (B / 64)) : 0;
+            if (cap && cap < B / 64) return;
+            const int nb = granted(copy_lean_kernel<3, B>, B, lds);
+            char name[200];
+            snprintf(name, sizeof name, "copy 1 GiB: copy_lean_kernel %dx1, lds %u B/block -> %d blocks = %d waves per CU",
+                     B, lds, nb, nb * B / 64);
+            const char* src = (const char*)buf[0];
+            char* dst = (char*)(ref ? buf[9] : buf[8]);
+            const unsigned blocks = (unsigned)(nvec / B);
+            vs.push_back({name, "copy", 2.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((copy_lean_kernel<3, B>), dim3(blocks), dim3(B), lds, st, src, dst, 0u,
+                                                 nvec, 0u);
+                              return hipGetLastError();
+                          }, dst, ref, bytes, {}});
+        };
+        add_copy(std::integral_constant<int, 512>(), 0, nullptr);
+        for (int cap : {0, 24, 16, 12, 8}) add_copy(std::integral_constant<int, 64>(), cap, buf[8]);
+        add_copy(std::integral_constant<int, 256>(), 0, buf[8]);
+        add_copy(std::integral_constant<int, 128>(), 0, buf[8]);
+        // conversions: fp32 -> bf16 (RNE) from buf[1] into buf[2]; bf16 -> fp32 back into buf[3]
+        const uint64_t count = bytes / 4;
+        auto add_conv = [&](auto st, auto dt, auto vconst, auto bconst, int cap, const char* label, const void* src,
+                            void* dst, void* ref, size_t dbytes) {
+            using ST = decltype(st);
+            using DT = decltype(dt);
+            constexpr unsigned V = decltype(vconst)::value;
+            constexpr int B = decltype(bconst)::value;
+            if (cap && cap < B / 64) return;
+            const unsigned lds = cap ? lds_for(cap / (B / 64)) : 0;
+            CArgs c{};
+            c.src = src;
+            c.dst = dst;
+            c.count = count;
+            c.trunc_from = count;
+            c.head = 0;
+            c.ngroups = count / 8;
+            const uint64_t blocks = std::min<uint64_t>((c.ngroups + B - 1) / B, 1u << 20);
+            const int nb = granted(convert_kernel<ST, DT, V, B>, B, lds);
+            char name[200];
+            snprintf(name, sizeof name, "%s convert_kernel %dx8, lds %u B/block -> %d blocks = %d waves per CU", label, B,
+                     lds, nb, nb * B / 64);
+            vs.push_back({name, label, 6.0 * count, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((convert_kernel<ST, DT, V, B>), dim3((unsigned)blocks), dim3(B), lds, st,
+                                                 c);
+                              return hipGetLastError();
+                          }, dst, ref, dbytes, {}});
+        };
+        using I256 = std::integral_constant<int, 256>;
+        using I64 = std::integral_constant<int, 64>;
+        using V2 = std::integral_constant<unsigned, V_BF16_RNE>;
+        using V0 = std::integral_constant<unsigned, 0u>;
+        void* nb16 = buf[2];
+        void* nb16b = static_cast<char*>(buf[2]) + bytes / 2;
+        add_conv(float(), bf16_tag(), V2(), I256(), 0, "fp32->bf16 2^28:", buf[1], nb16, nullptr, bytes / 2);
+        for (int cap : {0, 24, 16, 12}) add_conv(float(), bf16_tag(), V2(), I64(), cap, "fp32->bf16 2^28:", buf[1], nb16b, nb16, bytes / 2);
+        add_conv(bf16_tag(), float(), V0(), I256(), 0, "bf16->fp32 2^28:", nb16, buf[3], nullptr, bytes);
+        for (int cap : {0, 24, 16, 12}) add_conv(bf16_tag(), float(), V0(), I64(), cap, "bf16->fp32 2^28:", nb16, buf[4], buf[3], bytes);
     }
     if (which == "fank") {
         // the fan-in at 64-lane blocks over the input count and the wave cap
