@@ -55,6 +55,21 @@ for step in "$@"; do
                 i=$((i+1))
             done
             python tools/pmc_burst.py "$OUT/pmc_burst.json" "$OUT/pmcburst" > "$OUT/pmc_burst.out" 2>&1 ;;
+        occpmc)  # memory-side counters: round 2's and the current launch of C2 (in place) and C4 (pmcset)
+            for mode in ${OCCPMC_MODES:-pmcset}; do
+                i=0
+                for p in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum" \
+                         "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_CYCLE_sum"; do
+                    d="$GRAFT_REPO_ROOT/$OUT/occpmc_${mode}_$i"
+                    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $p --output-format csv -d "$d" -o occ -- \
+                        "$GRAFT_REPO_ROOT/tools/occupancy_sweep" 1024 2 4 $mode > "$d.out" 2> "$d.err")
+                    rc=$?; echo "=== occpmc $mode $i rc=$rc" | tee -a "$OUT/steps.log"
+                    [ $rc -eq 0 ] || exit $rc
+                    i=$((i+1))
+                done
+                python tools/pmc_burst.py "$OUT/occpmc_$mode.json" "$OUT/occpmc_$mode" \
+                    "rocprofv3 --pmc passes over tools/occupancy_sweep $mode (gpu_run.sh occpmc)" > "$OUT/occpmc_$mode.summary" 2>&1
+            done ;;
         fanpipe)
             run fanpipe 300 ./tools/fan_sweep 1024 ${SWEEP_ROUNDS:-4} 8 pipe ;;
         ldsstage)  # inputs staged through LDS by LDS-DMA vs the library's register path (C2, C3, C4)

@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -255,6 +255,27 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "pmcset") {
+        // one variant per kernel template, so rocprofv3's counter rows (which
+        // do not show the dynamic LDS) can be told apart: round 2's launch and
+        // the library's current one, for C2 in place and the 8-input fan-in
+        R2Args r{};
+        r.acc = r.out = buf[0];
+        r.in = buf[1];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        add_r2<float, 0u, 1024>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, 0, nullptr);
+        add_r2<float, 0u, 64>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, 24, nullptr);
+        KArgs a{};
+        for (int i = 0; i < 8; i++) a.in[i] = buf[i + 2 < 10 ? i + 2 : 0];
+        a.out = buf[2];
+        a.k = 8;
+        a.count = bytes / 4;
+        a.nvec = bytes / 16;
+        a.trunc_from = a.count;
+        add_fan<float, 0u, 1024>(vs, "C4 fp32 8-input 1 GiB in place:", a, bytes, 0, nullptr);
+        add_fan<float, 0u, 64>(vs, "C4 fp32 8-input 1 GiB in place:", a, bytes, 10, nullptr);
     }
     if (which == "copyconv") {
         // ccl_comp_copy's device kernel (1 GiB, nt loads and stores) and the

@@ -6,7 +6,10 @@ stalls, with the same derivations as tools/pmc_latency.py (128-B read and 64-B
 write requests; TCC_CYCLE summed over channels).  VERDICT r1 "next" #6 asked
 for the burst experiment's result with these counters beside it.
 
-  tools/pmc_burst.py OUT_JSON DIR_PREFIX        (DIR_PREFIX_0, _1, _2)
+  tools/pmc_burst.py OUT_JSON DIR_PREFIX [NOTE]  (DIR_PREFIX_0, _1, _2)
+
+Also used for tools/occupancy_sweep (gpu_run.sh occpmc): variants are told
+apart by template, grid and the LDS each workgroup reserves.
 """
 from __future__ import annotations
 
@@ -32,13 +35,15 @@ def main() -> None:
         path = glob.glob(f"{prefix}_{i}/*counter_collection.csv")[0]
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
-            if not any(k in n for k in ("burst_kernel", "reduce2_kernel", "fan_kernel")):
+            if not any(k in n for k in ("burst_kernel", "reduce2_kernel", "fan_kernel", "copy_lean_kernel",
+                                        "convert_kernel")):
                 continue
-            key = (short(n), int(r["Grid_Size"]) // int(r["Workgroup_Size"]))
+            # the LDS a launch reserves tells apart tools/occupancy_sweep's wave caps
+            key = (short(n), int(r["Grid_Size"]) // int(r["Workgroup_Size"]), int(r.get("LDS_Block_Size") or 0))
             vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     res = []
-    for (kname, grid), cs in sorted(vals.items()):
+    for (kname, grid, lds), cs in sorted(vals.items()):
         m = {k: statistics.median(v) for k, v in cs.items()}
         need = ("TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum", "TCC_CYCLE_sum", "TCC_EA0_RDREQ_LEVEL_sum",
                 "TCC_EA0_WRREQ_LEVEL_sum", "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum",
@@ -47,8 +52,8 @@ def main() -> None:
             continue
         rd, wr, cyc = m["TCC_EA0_RDREQ_sum"], m["TCC_EA0_WRREQ_sum"], m["TCC_CYCLE_sum"]
         res.append({
-            "kernel": kname, "workgroups": grid,
-            "launch_ms_median_under_pmc": round(statistics.median(dur[(kname, grid)]), 4),
+            "kernel": kname, "workgroups": grid, "lds_bytes_per_workgroup": lds,
+            "launch_ms_median_under_pmc": round(statistics.median(dur[(kname, grid, lds)]), 4),
             "read_bytes": int(rd * 128), "write_bytes": int(wr * 64),
             "avg_read_latency_cycles": round(m["TCC_EA0_RDREQ_LEVEL_sum"] / rd, 1),
             "avg_write_latency_cycles": round(m["TCC_EA0_WRREQ_LEVEL_sum"] / wr, 1),
@@ -58,10 +63,11 @@ def main() -> None:
             "read_dram_credit_stall_frac": round(m["TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"] / cyc, 4),
             "write_dram_credit_stall_frac": round(m["TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum"] / cyc, 4),
         })
-    doc = {"variants": res,
-           "_note": "One rocprofv3 --pmc pass per counter set over tools/burst_sweep 1024 MiB (gpu_run.sh burstpmc); "
-                    "medians over each variant's launches. Launches run slower under counter collection; the "
-                    "timed comparison is profiles/round2_burst/burst_sweep.jsonl."}
+    note = sys.argv[3] if len(sys.argv) > 3 else (
+        "One rocprofv3 --pmc pass per counter set over tools/burst_sweep 1024 MiB (gpu_run.sh burstpmc); "
+        "medians over each variant's launches. Launches run slower under counter collection; the "
+        "timed comparison is profiles/round2_burst/burst_sweep.jsonl.")
+    doc = {"variants": res, "_note": note}
     with open(out, "w") as f:
         f.write(json.dumps(doc, indent=1) + "\n")
     for r in res:
