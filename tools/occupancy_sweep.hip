@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -86,21 +86,21 @@ int granted(F kernel, int B, unsigned lds) {
     return nb;
 }
 
-template <typename Tag, unsigned V, int B>
+template <typename Tag, unsigned V, int B, int U = 1>
 void add_r2(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes, int cap_waves, void* ref) {
-    const unsigned blocks = (unsigned)(r.nvec / B);
+    const unsigned blocks = (unsigned)(r.nvec / ((uint64_t)B * U));
     const int waves = B / 64;
     const unsigned lds = cap_waves ? lds_for(cap_waves / waves) : 0;
-    if ((cap_waves && cap_waves < waves) || seen(std::string(group) + "r2/" + std::to_string(B) + "/" +
-                                                 std::to_string(lds) + (ref ? "" : "/ref")))
+    if ((cap_waves && cap_waves < waves) || seen(std::string(group) + "r2/" + std::to_string(B) + "x" +
+                                                 std::to_string(U) + "/" + std::to_string(lds) + (ref ? "" : "/ref")))
         return;
-    auto k = reduce2_kernel<Tag, OP_SUM, V, 1, B>;
+    auto k = reduce2_kernel<Tag, OP_SUM, V, U, B>;
     const int nb = granted(k, B, lds);
     char name[200];
-    snprintf(name, sizeof name, "%s reduce2_kernel %dx1, lds %u B/block -> %d blocks = %d waves per CU", group, B, lds,
-             nb, nb * waves);
+    snprintf(name, sizeof name, "%s reduce2_kernel %dx%d, lds %u B/block -> %d blocks = %d waves per CU", group, B, U,
+             lds, nb, nb * waves);
     vs.push_back({name, group, 3.0 * bytes, [r, blocks, lds](hipStream_t s) {
-                      hipLaunchKernelGGL((reduce2_kernel<Tag, OP_SUM, V, 1, B>), dim3(blocks), dim3(B), lds, s, r);
+                      hipLaunchKernelGGL((reduce2_kernel<Tag, OP_SUM, V, U, B>), dim3(blocks), dim3(B), lds, s, r);
                       return hipGetLastError();
                   }, r.out, ref, bytes, {}});
 }
@@ -255,6 +255,35 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "r2u") {
+        // one-wave tiles of one or two vectors per lane, in place, over the wave cap
+        void *la, *lb;
+        CK(hipMalloc(&la, bytes3));
+        CK(hipMalloc(&lb, bytes3));
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)la, bytes3 / 4, 0x1234u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)lb, bytes3 / 4, 0x4321u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        auto shapes = [&](auto tag, auto vconst, const char* g, R2Args r, size_t nbytes) {
+            using Tag = decltype(tag);
+            constexpr unsigned V = decltype(vconst)::value;
+            add_r2<Tag, V, 1024>(vs, g, r, nbytes, 0, nullptr);
+            for (int cap : {32, 28, 24, 20}) add_r2<Tag, V, 64>(vs, g, r, nbytes, cap, nullptr);
+            for (int cap : {24, 16, 12, 10, 8}) add_r2<Tag, V, 64, 2>(vs, g, r, nbytes, cap, nullptr);
+        };
+        R2Args r{};
+        r.acc = r.out = buf[0];
+        r.in = buf[1];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        shapes(float(), std::integral_constant<unsigned, 0u>(), "C2 fp32 sum 1 GiB in place:", r, bytes);
+        R2Args rb{};
+        rb.acc = rb.out = la;
+        rb.in = lb;
+        rb.nvec = bytes3 / 16;
+        rb.trunc_from = bytes3 / 2;
+        shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
     }
     if (which == "pmcset") {
         // one variant per kernel template, so rocprofv3's counter rows (which
