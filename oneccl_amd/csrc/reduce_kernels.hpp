@@ -1099,11 +1099,15 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(const char* __restrict__ s
     }
 }
 
-// The same copy as one tile per block, 512 lanes x one 16-byte vector, no loop
-// (reduce2_kernel's shape); the default grid (tools/copy_sweep.hip: 6.44 TB/s
-// median with nt loads and stores against 5.78 for copy_kernel<2>).
-// copy_kernel stays for a capped grid (mi_set_max_blocks).
-constexpr int kCopyBlock = 512;
+// The same copy as one tile per block, one 16-byte vector per lane, no loop
+// (reduce2_kernel's shape); the default grid.  One-wave (64-lane) tiles with
+// no residency cap: 1 GiB in 0.320 ms against 0.336 at round 2's 512 lanes
+// (-5 %; the 1-read/1-write stream keeps only 1 KiB per wave in flight, so
+// unlike the reduce kernels it wants every wave slot; tools/occupancy_sweep.hip
+// copyu / copyconv, profiles/round3_occupancy/).  Round 2's sweep
+// (tools/copy_sweep.hip) had 512 lanes at 6.44 TB/s against 5.78 for
+// copy_kernel<2>, which stays for a capped grid (mi_set_max_blocks).
+constexpr int kCopyBlock = 64;
 template <int MEM, int B = kCopyBlock>
 __global__ __launch_bounds__(B) void copy_lean_kernel(const char* __restrict__ src8, char* __restrict__ dst8,
                                                       uint32_t head, uint64_t nvec, uint32_t tail) {

@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,6 +54,21 @@ __global__ void count_diff(const uint32_t* a, const uint32_t* b, uint64_t nwords
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * blockDim.x)
         n += a[i] != b[i];
     if (n) atomicAdd(bad, n);
+}
+
+// copy with U 16-byte vectors per lane (all loads before the first store),
+// one tile of B*U vectors per block: the shape question for ccl_comp_copy
+template <int B, int U>
+__global__ __launch_bounds__(B) void copy_u_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                  uint64_t nvec) {
+    const uint64_t v0 = (uint64_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        if (v0 + (uint64_t)j * B < nvec) x[j] = __builtin_nontemporal_load(src + v0 + (uint64_t)j * B);
+#pragma unroll
+    for (int j = 0; j < U; j++)
+        if (v0 + (uint64_t)j * B < nvec) __builtin_nontemporal_store(x[j], dst + v0 + (uint64_t)j * B);
 }
 
 struct Variant {
@@ -255,6 +270,35 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "copyu") {
+        const uint64_t nvec = bytes / 16;
+        auto add_cu = [&](auto bconst, auto uconst, int cap, void* ref) {
+            constexpr int B = decltype(bconst)::value;
+            constexpr int U = decltype(uconst)::value;
+            if (cap && cap < B / 64) return;
+            const unsigned lds = cap ? lds_for(cap / (B / 64)) : 0;
+            const int nb = granted(copy_u_kernel<B, U>, B, lds);
+            char name[200];
+            snprintf(name, sizeof name, "copy 1 GiB: copy %dx%d, lds %u B/block -> %d blocks = %d waves per CU", B, U, lds,
+                     nb, nb * B / 64);
+            const u32x4* src = (const u32x4*)buf[0];
+            u32x4* dst = (u32x4*)(ref ? buf[9] : buf[8]);
+            const unsigned blocks = (unsigned)(nvec / (B * U));
+            vs.push_back({name, "copy", 2.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((copy_u_kernel<B, U>), dim3(blocks), dim3(B), lds, st, src, dst, nvec);
+                              return hipGetLastError();
+                          }, dst, ref, bytes, {}});
+        };
+        using I512 = std::integral_constant<int, 512>;
+        using I64 = std::integral_constant<int, 64>;
+        using U1 = std::integral_constant<int, 1>;
+        using U2 = std::integral_constant<int, 2>;
+        using U4 = std::integral_constant<int, 4>;
+        add_cu(I512(), U1(), 0, nullptr);  // the library's shape
+        add_cu(I64(), U1(), 0, buf[8]);
+        for (int cap : {0, 24, 16, 12}) add_cu(I64(), U2(), cap, buf[8]);
+        for (int cap : {0, 16, 12, 8}) add_cu(I64(), U4(), cap, buf[8]);
     }
     if (which == "r2u") {
         // one-wave tiles of one or two vectors per lane, in place, over the wave cap
