@@ -86,7 +86,7 @@ void add_convert(std::vector<Variant>& vs, const char* label, const void* src, v
     a.scalar_only = 0;
     const unsigned blocks = (unsigned)std::min<uint64_t>((a.ngroups + B - 1) / B, 1u << 20);
     const double t = (double)count * (sizeof(typename Tr<ST>::S) + sizeof(typename Tr<DT>::S));
-    vs.push_back({std::string("convert ") + label + " B=" + std::to_string(B) + (B == kBlock ? " (library)" : ""),
+    vs.push_back({std::string("convert ") + label + " B=" + std::to_string(B) + (B == kBlock ? " (round 2's block; the library now launches 64 lanes at 24 waves per CU, tools/occupancy_sweep.hip)" : ""),
                   [a, blocks](hipStream_t st) {
                       hipLaunchKernelGGL((convert_kernel<ST, DT, V, B>), dim3(blocks), dim3(B), 0, st, a);
                   }, {}, t});
@@ -114,11 +114,11 @@ int main(int argc, char** argv) {
         u32x4* d4 = reinterpret_cast<u32x4*>(dst);
         const uint64_t b_lib = (nvec + kBlock * 4 - 1) / (kBlock * 4);
         const unsigned b_lean = (unsigned)((nvec + kCopyBlock - 1) / kCopyBlock);
-        vs.push_back({"library copy_lean_kernel<3> 512x1 (nt ld, nt st)" + sfx, [=](hipStream_t st) {
+        vs.push_back({"library copy_lean_kernel<3> " + std::to_string(kCopyBlock) + "x1 (nt ld, nt st)" + sfx, [=](hipStream_t st) {
                           hipLaunchKernelGGL(copy_lean_kernel<3>, dim3(b_lean), dim3(kCopyBlock), 0, st, sp, dst, 0u,
                                              nvec, 0u);
                       }, {}});
-        vs.push_back({"library copy_lean_kernel<1> 512x1 (nt ld, plain st)" + sfx, [=](hipStream_t st) {
+        vs.push_back({"library copy_lean_kernel<1> " + std::to_string(kCopyBlock) + "x1 (nt ld, plain st)" + sfx, [=](hipStream_t st) {
                           hipLaunchKernelGGL(copy_lean_kernel<1>, dim3(b_lean), dim3(kCopyBlock), 0, st, sp, dst, 0u,
                                              nvec, 0u);
                       }, {}});
