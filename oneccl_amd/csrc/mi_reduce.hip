@@ -1925,6 +1925,15 @@ int mi_get_launch_config(int* block, int* unroll, int* max_blocks_out) {
     return 0;
 }
 
+int mi_get_residency(int device, int k, int* waves_per_cu, unsigned* lds_bytes) {
+    if (k < 0 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "k must be 0..16");
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) device = -1;
+    const int w = k == 2 ? kLeanWavesPerCU : k == 0 ? kConvWavesPerCU : fan_waves_per_cu(k);
+    if (waves_per_cu) *waves_per_cu = w;
+    if (lds_bytes) *lds_bytes = lds_per_cu(device) / (unsigned)w;
+    return 0;
+}
+
 int mi_set_max_blocks(int mb) {
     if (mb < 0) return fail(MI_E_INVALID, "max_blocks must be >= 0");
     g_max_blocks.store(mb, std::memory_order_relaxed);

@@ -161,3 +161,20 @@ def test_launch_config():
 
 def test_version():
     assert _lib.mi().mi_version() >= 100
+
+
+def test_residency_plan():
+    """The one-wave kernels' resident-wave caps: 24 per CU for
+    the 2-input kernel and the conversions, 16/12/10/8/6 for a fan-in of
+    <=4/<=6/<=8/<=12/<=16 inputs.  Without a GPU the LDS size is unknown and
+    no cap is reserved."""
+    m = _lib.mi()
+    w, lds = ctypes.c_int(), ctypes.c_uint()
+    want = {0: 24, 1: 16, 2: 24, 3: 16, 4: 16, 5: 12, 6: 12, 7: 10, 8: 10, 9: 8, 12: 8, 13: 6, 16: 6}
+    for k, waves in want.items():
+        assert m.mi_get_residency(-1, k, ctypes.byref(w), ctypes.byref(lds)) == 0
+        assert w.value == waves, (k, w.value)
+        if m.mi_device_count() == 0:
+            assert lds.value == 0
+    assert m.mi_get_residency(-1, 17, ctypes.byref(w), ctypes.byref(lds)) == -1
+    assert m.mi_get_residency(-1, -1, None, None) == -1

@@ -416,3 +416,18 @@ def test_fanin_beyond_32_bit_indices():
     _sync()
     got = ts[0].cpu().numpy()
     assert_same(got, exp, 0, f"n={n}")
+
+
+@pytest.mark.gpu
+def test_residency_caps_fit_the_device():
+    """On the GPU the caps are real: each one-wave workgroup reserves
+    LDS-per-CU / waves bytes, so exactly `waves` of them fit on a CU (MI355X:
+    160 KiB of LDS per CU, the size the caps were measured with)."""
+    import ctypes
+    m = _lib.mi()
+    w, lds = ctypes.c_int(), ctypes.c_uint()
+    for k in (0, 2, 3, 8, 16):
+        assert m.mi_get_residency(0, k, ctypes.byref(w), ctypes.byref(lds)) == 0
+        assert lds.value > 0, "the device reported no LDS size: kernels run uncapped"
+        per_cu = 160 * 1024
+        assert per_cu // lds.value == w.value, (k, w.value, lds.value)
