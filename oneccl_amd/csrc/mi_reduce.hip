@@ -179,19 +179,22 @@ constexpr int kLeanWavesPerCU = 24;
 constexpr int kFanBlock = 64;
 int fan_waves_per_cu(int k) { return k <= 4 ? 16 : k <= 6 ? 12 : k <= 8 ? 10 : k <= 12 ? 8 : 6; }
 
-// LDS bytes per CU of each device (read once per device; 0 = unknown: no cap)
+// LDS bytes per CU of each device (read once per device; 0 = unknown: no
+// cap).  Lock-free: every launch reads it, from any number of threads.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_lds_per_cu[kMaxDevices];  // 0 until read; read value + 1 after
+
 unsigned lds_per_cu(int device) {
-    static std::mutex mu;
-    static std::vector<int> cache;  // -1: not read yet
-    std::lock_guard<std::mutex> lk(mu);
-    if (device < 0) return 0;
-    if ((size_t)device >= cache.size()) cache.resize(device + 1, -1);
-    if (cache[device] < 0) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess) v = 0;
-        cache[device] = std::max(v, 0);
+    if (device < 0 || device >= kMaxDevices) return 0;
+    int v = g_lds_per_cu[device].load(std::memory_order_relaxed);
+    if (v == 0) {
+        int a = 0;
+        if (hipDeviceGetAttribute(&a, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
+            a = 0;
+        v = std::max(a, 0) + 1;
+        g_lds_per_cu[device].store(v, std::memory_order_relaxed);
     }
-    return (unsigned)cache[device];
+    return (unsigned)(v - 1);
 }
 
 // Dynamic LDS (never touched) for a one-wave block so that `waves` of them
