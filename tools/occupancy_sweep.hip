@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu|policy]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -69,6 +69,22 @@ __global__ __launch_bounds__(B) void copy_u_kernel(const u32x4* __restrict__ src
 #pragma unroll
     for (int j = 0; j < U; j++)
         if (v0 + (uint64_t)j * B < nvec) __builtin_nontemporal_store(x[j], dst + v0 + (uint64_t)j * B);
+}
+
+// 2-input fp32 sum through buffer ops with the cache-policy bits as template
+// arguments (aux: bit 0 sc0, bit 1 nt, bit 4 sc1), one-wave tiles
+template <int LA, int SA>
+__global__ __launch_bounds__(64) void r2pol_kernel(const void* in, void* io, uint64_t nvec) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    if (t0 >= nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(nvec - t0, 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(io, t0 * 16, bytes), off, 0, LA);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in, t0 * 16, bytes), off, 0, LA);
+    u32x4 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(a[e]) + __uint_as_float(b[e]));
+    __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(io, t0 * 16, bytes), off, 0, SA);
 }
 
 struct Variant {
@@ -270,6 +286,45 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "policy") {
+        // cache-policy bits of the one-wave 2-input kernel at 24 waves per CU, in place
+        R2Args r{};
+        r.acc = r.out = buf[0];
+        r.in = buf[1];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        add_r2<float, 0u, 64>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, 24, nullptr);  // the library
+        const unsigned lds = lds_for(24);
+        const uint64_t nvec = bytes / 16;
+        const unsigned blocks = (unsigned)(nvec / 64);
+        auto add_pol = [&](auto la, auto sa) {
+            constexpr int LA = decltype(la)::value, SA = decltype(sa)::value;
+            char name[160];
+            snprintf(name, sizeof name, "C2 fp32 sum 1 GiB in place: buffer 64x1 @24, load aux %d, store aux %d", LA, SA);
+            const void* in = buf[1];
+            void* io = buf[0];
+            vs.push_back({name, "pol", 3.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((r2pol_kernel<LA, SA>), dim3(blocks), dim3(64), lds, st, in, io, nvec);
+                              return hipGetLastError();
+                          }, io, nullptr, bytes, {}});
+        };
+        using A0 = std::integral_constant<int, 0>;
+        using A1 = std::integral_constant<int, 1>;
+        using A2 = std::integral_constant<int, 2>;
+        using A3 = std::integral_constant<int, 3>;
+        using A16 = std::integral_constant<int, 16>;
+        using A18 = std::integral_constant<int, 18>;
+        add_pol(A2(), A2());
+        add_pol(A2(), A0());
+        add_pol(A0(), A2());
+        add_pol(A2(), A16());
+        add_pol(A2(), A18());
+        add_pol(A18(), A2());
+        add_pol(A16(), A2());
+        add_pol(A1(), A2());
+        add_pol(A3(), A3());
+        add_pol(A18(), A18());
     }
     if (which == "copyu") {
         const uint64_t nvec = bytes / 16;
