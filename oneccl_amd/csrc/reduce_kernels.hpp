@@ -303,6 +303,18 @@ __device__ __forceinline__ void vstore(u32x4* p, u32x4 v) {
         *p = v;
 }
 
+// Buffer addressing (cdna_hip_programming.md T8/T20): one SGPR descriptor per
+// tile, built from kernel arguments and blockIdx only (wave-uniform), whose
+// range is the tile's valid bytes, so out-of-range lanes read zeros and their
+// stores are dropped.
+constexpr int kAuxNT = 2;      // buffer op aux bit 1: non-temporal (gfx950)
+constexpr int kAuxSC1NT = 18;  // sc1 + nt: the store drops the line from L2 instead of keeping it
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint64_t byte0, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(base) + byte0), (short)0,
+                                             (int)nbytes, 0x00020000);
+}
+
 template <typename S>
 struct alignas(16) Pack {
     S e[16 / sizeof(S)];
@@ -693,8 +705,15 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
     const size_t hb = (size_t)a.head * sizeof(S);
     const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.acc) + hb);
     const u32x4* p1 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in) + hb);
-    u32x4* po = reinterpret_cast<u32x4*>(static_cast<char*>(a.out) + hb);
-    const uint64_t v0 = (uint64_t)blk * (B * U) + threadIdx.x;
+    // the output through a buffer descriptor: stores with sc1 + nt drop each
+    // line from L2 as it is written; nt alone keeps it there, and the 2-input
+    // stream then ran 2.3-3.1 % slower (tools/occupancy_sweep.hip policy,
+    // profiles/round3_occupancy/).  The fan-in keeps nt (sc1 did not pay there).
+    const uint64_t t0 = (uint64_t)blk * (B * U);
+    const uint64_t tleft = a.nvec > t0 ? a.nvec - t0 : 0;
+    const uint32_t tbytes = (uint32_t)(tleft < (uint64_t)B * U ? tleft : (uint64_t)B * U) * 16u;
+    const __amdgpu_buffer_rsrc_t orsrc = tile_rsrc(a.out, hb + t0 * 16, tbytes);
+    const uint64_t v0 = t0 + threadIdx.x;
     u32x4 x[U], y[U];
     const bool full = v0 + (uint64_t)(U - 1) * B < a.nvec;
 #pragma unroll
@@ -708,10 +727,12 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
         const uint64_t v = v0 + (uint64_t)j * B;
         if (full || v < a.nvec) {
             const u32x4 xs[2] = {x[j], y[j]};
-            vstore<3>(po + v, fold_row<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from, [&](u32x4 (&r)[2]) {
-                          r[0] = vload<3>(p0 + v);
-                          r[1] = vload<3>(p1 + v);
-                      }));
+            __builtin_amdgcn_raw_buffer_store_b128(
+                fold_row<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from, [&](u32x4 (&r)[2]) {
+                    r[0] = vload<3>(p0 + v);
+                    r[1] = vload<3>(p1 + v);
+                }),
+                orsrc, (uint32_t)(v - t0) * 16u, 0, kAuxSC1NT);
         }
     }
 }
@@ -831,12 +852,6 @@ __global__ __launch_bounds__(B) void reducek_kernel(RKArgs a) {
 // read zeros and their stores are dropped by the range check: no guard
 // branches.  Lanes carry only a 32-bit byte offset.
 // ---------------------------------------------------------------------------
-constexpr int kAuxNT = 2;  // buffer op aux bit 1: non-temporal (gfx950)
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, uint64_t byte0, uint32_t nbytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(base) + byte0), (short)0,
-                                             (int)nbytes, 0x00020000);
-}
 
 // Fan-in with a runtime K (2..kMaxInputs): all K loads are issued before the
 // first combine (uniform branches on k only), then the left fold in the

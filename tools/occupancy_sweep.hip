@@ -87,6 +87,24 @@ __global__ __launch_bounds__(64) void r2pol_kernel(const void* in, void* io, uin
     __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(io, t0 * 16, bytes), off, 0, SA);
 }
 
+// 8-input fp32 sum fan-in through buffer ops, store policy as a template argument
+template <int SA>
+__global__ __launch_bounds__(64) void fanpol_kernel(KArgs a) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    if (t0 >= a.nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(a.nvec - t0, 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    u32x4 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(a.in[i], t0 * 16, bytes), off, 0, 2);
+    u32x4 r = x[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(x[i][e]) + __uint_as_float(r[e]));
+    __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, t0 * 16, bytes), off, 0, SA);
+}
+
 struct Variant {
     std::string name;
     std::string group;
@@ -309,22 +327,37 @@ int main(int argc, char** argv) {
                               return hipGetLastError();
                           }, io, nullptr, bytes, {}});
         };
-        using A0 = std::integral_constant<int, 0>;
-        using A1 = std::integral_constant<int, 1>;
         using A2 = std::integral_constant<int, 2>;
-        using A3 = std::integral_constant<int, 3>;
         using A16 = std::integral_constant<int, 16>;
         using A18 = std::integral_constant<int, 18>;
+        using A19 = std::integral_constant<int, 19>;
         add_pol(A2(), A2());
-        add_pol(A2(), A0());
-        add_pol(A0(), A2());
         add_pol(A2(), A16());
         add_pol(A2(), A18());
-        add_pol(A18(), A2());
-        add_pol(A16(), A2());
-        add_pol(A1(), A2());
-        add_pol(A3(), A3());
+        add_pol(A2(), A19());
         add_pol(A18(), A18());
+        // the 8-input fan-in at the library's cap (10 waves per CU), in place
+        KArgs f{};
+        for (int i = 0; i < 8; i++) f.in[i] = buf[i + 2];
+        f.out = buf[2];
+        f.k = 8;
+        f.count = bytes / 4;
+        f.nvec = nvec;
+        f.trunc_from = f.count;
+        add_fan<float, 0u, 64>(vs, "C4 fp32 8-input 1 GiB in place:", f, bytes, 10, nullptr);  // the library
+        const unsigned flds = lds_for(10);
+        auto add_fpol = [&](auto sa) {
+            constexpr int SA = decltype(sa)::value;
+            char name[160];
+            snprintf(name, sizeof name, "C4 fp32 8-input 1 GiB in place: buffer 64x1 @10, store aux %d", SA);
+            vs.push_back({name, "fpol", 9.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((fanpol_kernel<SA>), dim3(blocks), dim3(64), flds, st, f);
+                              return hipGetLastError();
+                          }, f.out, nullptr, bytes, {}});
+        };
+        add_fpol(A2());
+        add_fpol(A16());
+        add_fpol(A18());
     }
     if (which == "copyu") {
         const uint64_t nvec = bytes / 16;
