@@ -105,6 +105,17 @@ __global__ __launch_bounds__(64) void fanpol_kernel(KArgs a) {
     __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, t0 * 16, bytes), off, 0, SA);
 }
 
+// copy through buffer ops, store policy as a template argument, one-wave tiles
+template <int SA>
+__global__ __launch_bounds__(64) void copypol_kernel(const void* src, void* dst, uint64_t nvec) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    if (t0 >= nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(nvec - t0, 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(src, t0 * 16, bytes), off, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(x, tile_rsrc(dst, t0 * 16, bytes), off, 0, SA);
+}
+
 struct Variant {
     std::string name;
     std::string group;
@@ -358,6 +369,28 @@ int main(int argc, char** argv) {
         add_fpol(A2());
         add_fpol(A16());
         add_fpol(A18());
+        // the copy (1 GiB, buf[1] -> buf[9]), library launch and store policies
+        {
+            const char* cs = (const char*)buf[1];
+            char* cd = (char*)buf[9];
+            const unsigned cb = (unsigned)(nvec / kCopyBlock);
+            vs.push_back({"copy 1 GiB: library copy_lean_kernel<3>", "cpol", 2.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((copy_lean_kernel<3>), dim3(cb), dim3(kCopyBlock), 0, st, cs, cd, 0u, nvec,
+                                                 0u);
+                              return hipGetLastError();
+                          }, cd, nullptr, bytes, {}});
+            auto add_cpol = [&](auto sa) {
+                constexpr int SA = decltype(sa)::value;
+                char name[120];
+                snprintf(name, sizeof name, "copy 1 GiB: buffer 64x1, store aux %d", SA);
+                vs.push_back({name, "cpol", 2.0 * bytes, [=](hipStream_t st) {
+                                  hipLaunchKernelGGL((copypol_kernel<SA>), dim3(blocks), dim3(64), 0, st, cs, cd, nvec);
+                                  return hipGetLastError();
+                              }, cd, nullptr, bytes, {}});
+            };
+            add_cpol(A2());
+            add_cpol(A18());
+        }
     }
     if (which == "copyu") {
         const uint64_t nvec = bytes / 16;
