@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu|policy]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -146,7 +146,7 @@ int granted(F kernel, int B, unsigned lds) {
     return nb;
 }
 
-template <typename Tag, unsigned V, int B, int U = 1>
+template <typename Tag, unsigned V, int B, int U = 1, int OPX = OP_SUM>
 void add_r2(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes, int cap_waves, void* ref) {
     const unsigned blocks = (unsigned)(r.nvec / ((uint64_t)B * U));
     const int waves = B / 64;
@@ -154,13 +154,13 @@ void add_r2(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes,
     if ((cap_waves && cap_waves < waves) || seen(std::string(group) + "r2/" + std::to_string(B) + "x" +
                                                  std::to_string(U) + "/" + std::to_string(lds) + (ref ? "" : "/ref")))
         return;
-    auto k = reduce2_kernel<Tag, OP_SUM, V, U, B>;
+    auto k = reduce2_kernel<Tag, OPX, V, U, B>;
     const int nb = granted(k, B, lds);
     char name[200];
-    snprintf(name, sizeof name, "%s reduce2_kernel %dx%d, lds %u B/block -> %d blocks = %d waves per CU", group, B, U,
-             lds, nb, nb * waves);
+    snprintf(name, sizeof name, "%s reduce2_kernel<op %d> %dx%d, lds %u B/block -> %d blocks = %d waves per CU", group,
+             OPX, B, U, lds, nb, nb * waves);
     vs.push_back({name, group, 3.0 * bytes, [r, blocks, lds](hipStream_t s) {
-                      hipLaunchKernelGGL((reduce2_kernel<Tag, OP_SUM, V, U, B>), dim3(blocks), dim3(B), lds, s, r);
+                      hipLaunchKernelGGL((reduce2_kernel<Tag, OPX, V, U, B>), dim3(blocks), dim3(B), lds, s, r);
                       return hipGetLastError();
                   }, r.out, ref, bytes, {}});
 }
@@ -315,6 +315,28 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "c5ops") {
+        // the library's 2-input launch over dtypes and ops, same buffers, in place
+        auto one = [&](auto tag, auto opc, const char* g, void* acc, void* in, int cap = 24) {
+            using Tag = decltype(tag);
+            constexpr int OPX = decltype(opc)::value;
+            R2Args r{};
+            r.acc = r.out = acc;
+            r.in = in;
+            r.nvec = bytes / 16;
+            r.trunc_from = bytes / sizeof(typename Tr<Tag>::S);
+            add_r2<Tag, 0u, 64, 1, OPX>(vs, g, r, bytes, cap, nullptr);
+        };
+        one(float(), std::integral_constant<int, OP_SUM>(), "fp32 sum:", buf[0], buf[1]);
+        one(int32_t(), std::integral_constant<int, OP_SUM>(), "int32 sum:", buf[2], buf[3]);
+        one(int32_t(), std::integral_constant<int, OP_MAX>(), "int32 max:", buf[4], buf[5]);
+        one(int64_t(), std::integral_constant<int, OP_PROD>(), "int64 prod:", buf[6], buf[7]);
+        one(int32_t(), std::integral_constant<int, OP_MAX>(), "int32 max (fp32 sum's buffers):", buf[0], buf[1]);
+        one(int64_t(), std::integral_constant<int, OP_SUM>(), "int64 sum:", buf[6], buf[7]);
+        for (int cap : {28, 32, 0}) one(int64_t(), std::integral_constant<int, OP_PROD>(), "int64 prod:", buf[6], buf[7], cap);
+        for (int cap : {28, 32}) one(float(), std::integral_constant<int, OP_PROD>(), "fp32 prod:", buf[0], buf[1], cap);
+        one(float(), std::integral_constant<int, OP_PROD>(), "fp32 prod:", buf[0], buf[1], 24);
     }
     if (which == "policy") {
         // cache-policy bits of the one-wave 2-input kernel at 24 waves per CU, in place
