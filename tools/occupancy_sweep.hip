@@ -116,6 +116,25 @@ __global__ __launch_bounds__(64) void copypol_kernel(const void* src, void* dst,
     __builtin_amdgcn_raw_buffer_store_b128(x, tile_rsrc(dst, t0 * 16, bytes), off, 0, SA);
 }
 
+// the same fan-in with global (flat) loads and stores, guarded per lane
+template <int NTST>
+__global__ __launch_bounds__(64) void fanglob_kernel(KArgs a) {
+    const uint64_t v = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (v >= a.nvec) return;
+    u32x4 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = __builtin_nontemporal_load(static_cast<const u32x4*>(a.in[i]) + v);
+    u32x4 r = x[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(x[i][e]) + __uint_as_float(r[e]));
+    if (NTST)
+        __builtin_nontemporal_store(r, static_cast<u32x4*>(a.out) + v);
+    else
+        static_cast<u32x4*>(a.out)[v] = r;
+}
+
 struct Variant {
     std::string name;
     std::string group;
@@ -391,6 +410,11 @@ int main(int argc, char** argv) {
         add_fpol(A2());
         add_fpol(A16());
         add_fpol(A18());
+        vs.push_back({"C4 fp32 8-input 1 GiB in place: global 64x1 @10, nt loads, nt stores", "fglob", 9.0 * bytes,
+                      [=](hipStream_t st) {
+                          hipLaunchKernelGGL((fanglob_kernel<1>), dim3(blocks), dim3(64), flds, st, f);
+                          return hipGetLastError();
+                      }, f.out, nullptr, bytes, {}});
         // the copy (1 GiB, buf[1] -> buf[9]), library launch and store policies
         {
             const char* cs = (const char*)buf[1];
