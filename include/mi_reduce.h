@@ -331,8 +331,9 @@ int mi_get_launch_config(int* block, int* unroll, int* max_blocks);
  * 3..16 the fan-in, k = 0 the array conversions.  *waves_per_cu = the
  * resident waves per CU the launch is sized for; *lds_bytes = the dynamic
  * LDS (never touched) each one-wave workgroup reserves to cap it there, 0
- * when the device does not report its LDS per CU (no cap then).  DESIGN.md
- * §5; tools/occupancy_sweep.hip measured the caps.                        */
+ * when the device does not report its LDS per CU or MI_REDUCE_WAVE_CAP=0
+ * (no cap then).  DESIGN.md §5; tools/occupancy_sweep.hip measured the
+ * caps.                                                                    */
 int mi_get_residency(int device, int k, int* waves_per_cu, unsigned* lds_bytes);
 /* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS).  Under a
  * cap the reduce, copy and conversion kernels stride over the buffer.     */

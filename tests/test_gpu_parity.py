@@ -431,3 +431,40 @@ def test_residency_caps_fit_the_device():
         assert lds.value > 0, "the device reported no LDS size: kernels run uncapped"
         per_cu = 160 * 1024
         assert per_cu // lds.value == w.value, (k, w.value, lds.value)
+
+
+@pytest.mark.gpu
+def test_wave_cap_off_same_bits():
+    """MI_REDUCE_WAVE_CAP=0 (read once per process, so in a child): no LDS is
+    reserved, and the 2-input and fan-in kernels give the same bits."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import ctypes, numpy as np, torch
+from oneccl_amd import _lib
+import oracle
+m = _lib.mi()
+w, lds = ctypes.c_int(), ctypes.c_uint()
+assert m.mi_get_residency(0, 8, ctypes.byref(w), ctypes.byref(lds)) == 0 and lds.value == 0, lds.value
+rng = np.random.default_rng(5)
+n = (1 << 22) + 37
+xs = [rng.standard_normal(n).astype(np.float32) for _ in range(8)]
+exp2 = xs[0].copy(); oracle.comp_reduce_mt(xs[1], exp2, 9, 0, 8)
+exp8 = xs[0].copy()
+for x in xs[1:]: oracle.comp_reduce_mt(x, exp8, 9, 0, 8)
+ts = [torch.from_numpy(x).cuda() for x in xs]
+s = torch.cuda.current_stream().cuda_stream
+a = ts[0].clone()
+_lib.check(m.mi_reduce(ts[1].data_ptr(), a.data_ptr(), n, 9, 0, 0, s))
+arr = _lib.void_ptr_array([t.data_ptr() for t in ts])
+_lib.check(m.mi_reduce_multi(arr, 8, ts[0].data_ptr(), n, 9, 0, 0, s))
+torch.cuda.synchronize()
+assert a.cpu().numpy().view(np.uint32).tolist() == exp2.view(np.uint32).tolist()
+assert ts[0].cpu().numpy().view(np.uint32).tolist() == exp8.view(np.uint32).tolist()
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MI_REDUCE_WAVE_CAP="0", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
