@@ -81,6 +81,8 @@ for step in "$@"; do
             run occr2 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 r2ab ;;
         occcopy)  # the copy and conversion kernels: block size and wave cap
             run occcopy 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 copyconv ;;
+        fanu)  # the 8-input fan-in with 1, 2 or 4 vectors per lane, load order, wave cap
+            run fanu 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 fanu ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)

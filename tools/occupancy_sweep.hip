@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|fanu|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -133,6 +133,47 @@ __global__ __launch_bounds__(64) void fanglob_kernel(KArgs a) {
         __builtin_nontemporal_store(r, static_cast<u32x4*>(a.out) + v);
     else
         static_cast<u32x4*>(a.out)[v] = r;
+}
+
+// the 8-input fp32 sum fan-in with U vectors per lane: one wave owns a tile
+// of 64*U vectors of every input (U KiB contiguous per stream), the lane's
+// j-th vector at tile + j*64 + lane.  IM: loads issued input-major (each
+// stream's U requests back to back) instead of vector-major.
+template <int U, bool IM>
+__global__ __launch_bounds__(64) void fanu_kernel(KArgs a) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64 * U;
+    if (t0 >= a.nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(a.nvec - t0, 64 * U) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const void* in[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        in[i] = a.in[i];
+        asm volatile("" ::"s"(in[i]));
+    }
+    u32x4 x[8][U];
+    if (IM) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                x[i][j] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], t0 * 16, bytes), off + j * 1024u, 0, 2);
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; j++)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                x[i][j] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], t0 * 16, bytes), off + j * 1024u, 0, 2);
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        u32x4 r = x[0][j];
+#pragma unroll
+        for (int i = 1; i < 8; i++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(x[i][j][e]) + __uint_as_float(r[e]));
+        __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, t0 * 16, bytes), off + j * 1024u, 0, kAuxNT);
+    }
 }
 
 struct Variant {
@@ -614,6 +655,47 @@ int main(int argc, char** argv) {
                 b.out = buf[9];
                 for (int cap : {0, 32, 24, 21, 16, 12, 10, 8, 6, 4}) add_fan<float, 0u, 64, 16>(vs, g, b, bytes, cap, a.out);
             }
+        }
+    }
+    if (which == "fanu") {
+        // the 8-input fan-in with 1, 2 or 4 vectors per lane, over the wave cap
+        KArgs a{};
+        for (int i = 0; i < 8; i++) a.in[i] = buf[i];
+        a.out = buf[8];
+        a.k = 8;
+        a.count = bytes / 4;
+        a.nvec = bytes / 16;
+        a.trunc_from = a.count;
+        add_fan<float, 0u, 64>(vs, "C4 fp32 8-input 1 GiB:", a, bytes, 10, nullptr);  // the library's launch
+        KArgs b = a;
+        b.out = buf[9];
+        auto add_u = [&](auto uconst, auto imconst, int cap) {
+            constexpr int U = decltype(uconst)::value;
+            constexpr bool IM = decltype(imconst)::value;
+            const unsigned lds = lds_for(cap);
+            const int nb = granted(fanu_kernel<U, IM>, 64, lds);
+            char name[200];
+            snprintf(name, sizeof name, "C4 fp32 8-input 1 GiB: fanu 64x%d %s, lds %u B/block -> %d waves per CU", U,
+                     IM ? "input-major" : "vector-major", lds, nb);
+            const unsigned blocks = (unsigned)(b.nvec / (64 * U));
+            vs.push_back({name, "fanu", 9.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL((fanu_kernel<U, IM>), dim3(blocks), dim3(64), lds, st, b);
+                              return hipGetLastError();
+                          }, b.out, a.out, bytes, {}});
+        };
+        using U1 = std::integral_constant<int, 1>;
+        using U2 = std::integral_constant<int, 2>;
+        using U4 = std::integral_constant<int, 4>;
+        using T = std::true_type;
+        using F = std::false_type;
+        add_u(U1(), F(), 10);
+        for (int cap : {12, 10, 8, 6, 5, 4}) {
+            add_u(U2(), F(), cap);
+            add_u(U2(), T(), cap);
+        }
+        for (int cap : {8, 6, 5, 4, 3, 2}) {
+            add_u(U4(), F(), cap);
+            add_u(U4(), T(), cap);
         }
     }
     if (which == "c4bf") {
