@@ -83,6 +83,8 @@ for step in "$@"; do
             run occcopy 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-10} 8 copyconv ;;
         fanu)  # the 8-input fan-in with 1, 2 or 4 vectors per lane, load order, wave cap
             run fanu 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 fanu ;;
+        xcd)  # one-wave tiles handed to each XCD in runs of G consecutive tiles (C2 in place, C4)
+            run xcd 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 xcd ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)

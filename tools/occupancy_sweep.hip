@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|fanu|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|fanu|xcd|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -174,6 +174,53 @@ __global__ __launch_bounds__(64) void fanu_kernel(KArgs a) {
             for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(x[i][j][e]) + __uint_as_float(r[e]));
         __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, t0 * 16, bytes), off + j * 1024u, 0, kAuxNT);
     }
+}
+
+// Workgroups are handed to the 8 XCDs round robin (block b -> XCD b % 8).
+// remap_tile gives XCD x runs of G consecutive tiles: the j-th block an XCD
+// receives takes tile (j / G) * 8G + x * G + j % G (G = 1: the identity).
+// nblocks must be a multiple of 8G.
+__device__ __forceinline__ uint64_t remap_tile(uint64_t b, uint64_t G) {
+    const uint64_t x = b & 7, j = b >> 3;
+    return (j / G) * 8 * G + x * G + j % G;
+}
+
+// 2-input fp32 sum in place with the library's cache policy (nt loads,
+// sc1 + nt stores), tiles remapped per XCD
+__global__ __launch_bounds__(64) void r2xcd_kernel(const void* in, void* io, uint64_t nvec, uint64_t G) {
+    const uint64_t t0 = remap_tile(blockIdx.x, G) * 64;
+    if (t0 >= nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(nvec - t0, 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(io, t0 * 16, bytes), off, 0, 2);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in, t0 * 16, bytes), off, 0, 2);
+    u32x4 r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(a[e]) + __uint_as_float(b[e]));
+    __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(io, t0 * 16, bytes), off, 0, 18);
+}
+
+// 8-input fp32 sum fan-in (nt loads and stores), tiles remapped per XCD
+__global__ __launch_bounds__(64) void fanxcd_kernel(KArgs a, uint64_t G) {
+    const uint64_t t0 = remap_tile(blockIdx.x, G) * 64;
+    if (t0 >= a.nvec) return;
+    const uint32_t bytes = (uint32_t)std::min<uint64_t>(a.nvec - t0, 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const void* in[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        in[i] = a.in[i];
+        asm volatile("" ::"s"(in[i]));
+    }
+    u32x4 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(in[i], t0 * 16, bytes), off, 0, 2);
+    u32x4 r = x[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) r[e] = __float_as_uint(__uint_as_float(x[i][e]) + __uint_as_float(r[e]));
+    __builtin_amdgcn_raw_buffer_store_b128(r, tile_rsrc(a.out, t0 * 16, bytes), off, 0, 2);
 }
 
 struct Variant {
@@ -696,6 +743,48 @@ int main(int argc, char** argv) {
         for (int cap : {8, 6, 5, 4, 3, 2}) {
             add_u(U4(), F(), cap);
             add_u(U4(), T(), cap);
+        }
+    }
+    if (which == "xcd") {
+        // one-wave tiles remapped so each XCD takes runs of G consecutive
+        // tiles (G = 1 is the hardware's round robin, the library's order)
+        const uint64_t nvec = bytes / 16;
+        const unsigned blocks = (unsigned)(nvec / 64);
+        R2Args r{};
+        r.acc = r.out = buf[0];
+        r.in = buf[1];
+        r.nvec = nvec;
+        r.trunc_from = bytes / 4;
+        add_r2<float, 0u, 64>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, 24, nullptr);  // the library
+        const unsigned lds24 = lds_for(24), lds10 = lds_for(10);
+        const uint64_t gs[] = {1, 2, 4, 16, 64, 1024, blocks / 8};
+        for (uint64_t G : gs) {
+            char name[160];
+            snprintf(name, sizeof name, "C2 fp32 sum 1 GiB in place: xcd runs of %llu tiles, 64x1 @24",
+                     (unsigned long long)G);
+            const void* in = buf[1];
+            void* io = buf[0];
+            vs.push_back({name, "r2xcd", 3.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL(r2xcd_kernel, dim3(blocks), dim3(64), lds24, st, in, io, nvec, G);
+                              return hipGetLastError();
+                          }, io, nullptr, bytes, {}});
+        }
+        KArgs f{};
+        for (int i = 0; i < 8; i++) f.in[i] = buf[i + 2];
+        f.out = buf[2];
+        f.k = 8;
+        f.count = bytes / 4;
+        f.nvec = nvec;
+        f.trunc_from = f.count;
+        add_fan<float, 0u, 64>(vs, "C4 fp32 8-input 1 GiB in place:", f, bytes, 10, nullptr);  // the library
+        for (uint64_t G : gs) {
+            char name[160];
+            snprintf(name, sizeof name, "C4 fp32 8-input 1 GiB in place: xcd runs of %llu tiles, 64x1 @10",
+                     (unsigned long long)G);
+            vs.push_back({name, "fanxcd", 9.0 * bytes, [=](hipStream_t st) {
+                              hipLaunchKernelGGL(fanxcd_kernel, dim3(blocks), dim3(64), lds10, st, f, G);
+                              return hipGetLastError();
+                          }, f.out, nullptr, bytes, {}});
         }
     }
     if (which == "c4bf") {
