@@ -151,6 +151,25 @@ def build_latency(force: bool = False) -> Path:
     return out
 
 
+def build_pointer_kind_probe(force: bool = False) -> Path:
+    """Probe: pointer classification cost against concurrent threads."""
+    out = ROOT / "tools" / "pointer_kind_probe"
+    src = ROOT / "tools" / "pointer_kind_probe.cpp"
+    if src.exists() and (force or _stale(out, [src])):
+        _run([_hipcc(), "-O2", "-std=c++17", "-o", str(out), str(src), "-pthread", "-lhsa-runtime64"])
+    return out
+
+
+def build_small_workers(force: bool = False) -> Path:
+    """Probe: small host reduces through the drop-in from T threads at once."""
+    out = ROOT / "tools" / "small_workers"
+    src = ROOT / "tools" / "small_workers.cpp"
+    if src.exists() and (force or _stale(out, [src, LIB / "libccl_comp_hip.so"])):
+        _run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", "-o", str(out), str(src), f"-L{LIB}",
+              "-lccl_comp_hip", "-Wl,-rpath,$ORIGIN/../oneccl_amd/lib", "-pthread"])
+    return out
+
+
 def build_segv_trace(force: bool = False) -> Path:
     """Diagnostic: tools/libsegv_trace.so prints a native backtrace on SIGSEGV."""
     out = ROOT / "tools" / "libsegv_trace.so"
@@ -239,6 +258,8 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_lds_stage_sweep()
     build_occupancy_sweep()
     build_latency()
+    build_pointer_kind_probe()
+    build_small_workers()
     build_segv_trace()
     if asan:
         build_asan(force)

@@ -180,9 +180,14 @@ struct MiEnv {
     HostMax host_max;  // CCL_COMP_HOST_MAX_BYTES, CCL_COMP_HOST_MAX_PINNED_BYTES
 };
 
-std::mutex g_env_mu;
-MiEnv g_env;
-bool g_env_ready = false;
+// The parsed environment is an immutable snapshot published through an
+// atomic pointer: every reduce reads it several times, from up to
+// CCL_WORKER_COUNT threads at once, so the read takes no lock.  A reload
+// (the standalone test hook mi_ccl_env_reload) publishes a new snapshot and
+// keeps the old ones alive, since a reader may still hold a reference.
+std::mutex g_env_mu;  // serialises parsing and publishing
+std::atomic<const MiEnv*> g_env_cur{nullptr};
+std::vector<std::unique_ptr<MiEnv>> g_env_all;  // every snapshot published (under g_env_mu)
 
 void cpuid(uint32_t leaf, uint32_t sub, uint32_t r[4]) {
 #if defined(__x86_64__) || defined(__i386__)
@@ -220,7 +225,8 @@ std::set<ccl_fp16_impl_type> fp16_impl_types() {
 }
 
 void parse_env_locked() {
-    MiEnv e;
+    std::unique_ptr<MiEnv> snap(new MiEnv);
+    MiEnv& e = *snap;
     e.bf16 = *bf16_impl_types().rbegin();
     if (const char* v = getenv("CCL_BF16")) {
         bool found = false;
@@ -246,14 +252,15 @@ void parse_env_locked() {
         MI_CCL_THROW("unsupported FP16 impl type: " + fp16_impl_names[e.fp16]);
     if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) e.device = atoi(v);
     e.host_max = parse_host_max();
-    g_env = e;
-    g_env_ready = true;
+    g_env_all.push_back(std::move(snap));
+    g_env_cur.store(g_env_all.back().get(), std::memory_order_release);
 }
 
 const MiEnv& env() {
+    if (const MiEnv* e = g_env_cur.load(std::memory_order_acquire)) return *e;
     std::lock_guard<std::mutex> g(g_env_mu);
-    if (!g_env_ready) parse_env_locked();
-    return g_env;
+    if (!g_env_cur.load(std::memory_order_relaxed)) parse_env_locked();
+    return *g_env_cur.load(std::memory_order_relaxed);
 }
 
 }  // namespace
@@ -386,44 +393,51 @@ const Roctx& roctx() {
 // CCL_COMP_HIP_SHARD_DEVICES=<d0>,<d1>,...: host-resident reduces are split by
 // element range over these GPUs, each shard over its own PCIe link
 // (mi_reduce_multi_sync_sharded).  Unset or one device: a single GPU.
+// Read on every synchronous reduce: a published snapshot, as env() above.
 std::mutex g_shard_mu;
-std::vector<int> g_shard_devs;
-bool g_shard_ready = false;
+std::atomic<const std::vector<int>*> g_shard_cur{nullptr};
+std::vector<std::unique_ptr<std::vector<int>>> g_shard_all;  // under g_shard_mu
 
-std::vector<int> shard_devices() {
+const std::vector<int>& shard_devices() {
+    if (const std::vector<int>* d = g_shard_cur.load(std::memory_order_acquire)) return *d;
     std::lock_guard<std::mutex> g(g_shard_mu);
-    if (!g_shard_ready) {
-        g_shard_devs.clear();
-        if (const char* v = getenv("CCL_COMP_HIP_SHARD_DEVICES")) {
-            std::string cur;
-            for (const char* c = v;; c++) {
-                if (*c == ',' || *c == 0) {
-                    if (!cur.empty()) g_shard_devs.push_back(atoi(cur.c_str()));
-                    cur.clear();
-                    if (!*c) break;
-                } else {
-                    cur += *c;
-                }
+    if (const std::vector<int>* d = g_shard_cur.load(std::memory_order_relaxed)) return *d;
+    std::unique_ptr<std::vector<int>> devs(new std::vector<int>);
+    if (const char* v = getenv("CCL_COMP_HIP_SHARD_DEVICES")) {
+        std::string cur;
+        for (const char* c = v;; c++) {
+            if (*c == ',' || *c == 0) {
+                if (!cur.empty()) devs->push_back(atoi(cur.c_str()));
+                cur.clear();
+                if (!*c) break;
+            } else {
+                cur += *c;
             }
         }
-        g_shard_ready = true;
     }
-    return g_shard_devs;
+    g_shard_all.push_back(std::move(devs));
+    g_shard_cur.store(g_shard_all.back().get(), std::memory_order_release);
+    return *g_shard_all.back();
 }
 
 #ifndef MI_ONECCL_TREE
 void shard_env_reload() {  // standalone only: oneCCL's env is read once, at init
     std::lock_guard<std::mutex> g(g_shard_mu);
-    g_shard_ready = false;
+    g_shard_cur.store(nullptr, std::memory_order_release);
 }
 #endif
 
 // Host kind of a set of operands: 0 = some operand is device memory,
 // 1 = all pinned host memory, 2 = host memory, some of it pageable.
+// Each distinct pointer is classified once: the lookup
+// (hipPointerGetAttributes) takes a runtime-wide lock, so with several worker
+// threads reducing small host chunks it is the one step that serialises
+// them, and the in-place form passes inout both as out and as the first input.
 int host_kind(const void* const* ptrs, int n, const void* out) {
     int dev = -1, kind = mi_pointer_kind(out, &dev);
     if (kind == 0) return 0;
     for (int i = 0; i < n; i++) {
+        if (ptrs[i] == out) continue;
         const int k = mi_pointer_kind(ptrs[i], &dev);
         if (k == 0) return 0;
         kind = std::max(kind, k);
@@ -640,7 +654,7 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     // 0: some operand is device memory (or the dispatcher is off), 1: all
     // pinned, 2: host memory, some of it pageable
     const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
-    const std::vector<int> devs = shard_devices();
+    const std::vector<int>& devs = shard_devices();
     const HostCall call(kind != 0);  // the thread counts among the host-bucket workers
     if (kind != 0) {
         const size_t lim = kind == 1 ? m.pinned : m.pageable;
