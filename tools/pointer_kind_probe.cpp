@@ -43,8 +43,31 @@ int main() {
                 info.size = sizeof(info);
                 (void)hsa_amd_pointer_info(ptr(t), &info, nullptr, nullptr, nullptr);
             });
-            printf("{\"threads\": %d, \"memory\": \"%s\", \"hipPointerGetAttributes_us\": %.3f, \"hsa_amd_pointer_info_us\": %.3f}\n",
-                   T, kind == 0 ? "pageable" : kind == 1 ? "pinned" : "device", a, b);
+            int ok_range = 0, ok_attr = 0;
+            const double c = run(T, [&](int t) {
+                hipDeviceptr_t base;
+                size_t size = 0;
+                if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr(t)) != hipSuccess) (void)hipGetLastError();
+            });
+            const double d = run(T, [&](int t) {
+                unsigned int mt = 0;
+                if (hipPointerGetAttribute(&mt, HIP_POINTER_ATTRIBUTE_MEMORY_TYPE, (hipDeviceptr_t)ptr(t)) != hipSuccess)
+                    (void)hipGetLastError();
+            });
+            {
+                hipDeviceptr_t base;
+                size_t size = 0;
+                ok_range = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr(0)) == hipSuccess;
+                (void)hipGetLastError();
+                unsigned int mt = 0;
+                ok_attr = hipPointerGetAttribute(&mt, HIP_POINTER_ATTRIBUTE_MEMORY_TYPE, (hipDeviceptr_t)ptr(0)) == hipSuccess;
+                (void)hipGetLastError();
+            }
+            printf("{\"threads\": %d, \"memory\": \"%s\", \"hipPointerGetAttributes_us\": %.3f, \"hsa_amd_pointer_info_us\": %.3f, "
+                   "\"hipMemGetAddressRange_us\": %.3f, \"hipMemGetAddressRange_ok\": %d, \"hipPointerGetAttribute_memtype_us\": %.3f, "
+                   "\"hipPointerGetAttribute_ok\": %d}\n",
+                   T, kind == 0 ? "pageable" : kind == 1 ? "pinned" : "device", a, b, c, ok_range, d, ok_attr);
+            fflush(stdout);
         }
     }
 }

@@ -25,4 +25,5 @@ int main(int argc, char** argv) {
     for (auto& x : th) x.join();
     std::sort(us.begin(), us.end());
     printf("T=%d n=%zu median %.3f us/call max %.3f\n", T, n, us[T / 2], us[T - 1]);
+    fflush(stdout);
 }
