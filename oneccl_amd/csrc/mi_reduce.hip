@@ -329,32 +329,8 @@ Kern pick(int dt, int op, unsigned v) {
 // ---------------------------------------------------------------------------
 enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
 
-// MI_REDUCE_PTR_LOOKUP=range: a pointer HIP holds no allocation for
-// (hipMemGetAddressRange fails) is taken as pageable host memory without the
-// full attribute lookup, whose not-found path serialises concurrent callers
-// (tools/pointer_kind_probe.cpp).  Under evaluation.
-std::atomic<int> g_ptr_lookup{-1};  // -1 = not yet read from env; 0 = attributes only; 1 = range first
-
-bool ptr_lookup_range() {
-    int v = g_ptr_lookup.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char* s = getenv("MI_REDUCE_PTR_LOOKUP");
-        v = (s && strcmp(s, "range") == 0) ? 1 : 0;
-        g_ptr_lookup.store(v, std::memory_order_relaxed);
-    }
-    return v == 1;
-}
-
 // `devptr` (optional): the device-visible address of a pinned host pointer.
 PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
-    if (ptr_lookup_range()) {
-        hipDeviceptr_t base = nullptr;
-        size_t size = 0;
-        if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
-            (void)hipGetLastError();
-            return PK_PAGEABLE;
-        }
-    }
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
