@@ -102,6 +102,18 @@ int mi_ccl_comp_split_take_gpu_alone(int pinned);
 int mi_ccl_comp_split_feed(int pinned, size_t count, size_t head, double t_head, double t_tail);
 /* The dispatcher's thresholds and default shares in force (after env).     */
 int mi_ccl_comp_host_max(size_t* pageable, size_t* pinned, double* share, double* share_pinned);
+/* Host buffer registry.  A caller that owns host memory (oneCCL's schedule
+ * buffers: sched->alloc_buffer, src/sched/buffer/buffer_manager.cpp) may
+ * declare [ptr, ptr + bytes) as host memory until it unregisters it; an
+ * operand lying wholly inside a registered buffer is taken as pageable host
+ * memory without asking HIP, whose lookup of pageable pointers serialises
+ * concurrent workers.  Registered memory must not be device
+ * memory; pinned memory registered here is treated as pageable (staged, not
+ * read in place).  Buffers may not overlap.  0 or an MI_E_* code.          */
+int mi_ccl_comp_register_host_buffer(const void* ptr, size_t bytes);
+int mi_ccl_comp_unregister_host_buffer(const void* ptr);
+/* Pointer lookups through HIP made by the calling thread so far.  Diagnostic. */
+size_t mi_ccl_comp_pointer_lookups(void);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

@@ -112,6 +112,9 @@ SHIM_API = [
     ("mi_ccl_comp_split_take_gpu_alone", c_int, [c_int]),
     ("mi_ccl_comp_split_feed", c_int, [c_int, c_size_t, c_size_t, c_double, c_double]),
     ("mi_ccl_comp_host_max", c_int, [POINTER(c_size_t), POINTER(c_size_t), POINTER(c_double), POINTER(c_double)]),
+    ("mi_ccl_comp_register_host_buffer", c_int, [c_void_p, c_size_t]),
+    ("mi_ccl_comp_unregister_host_buffer", c_int, [c_void_p]),
+    ("mi_ccl_comp_pointer_lookups", c_size_t, []),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -429,23 +430,61 @@ void shard_env_reload() {  // standalone only: oneCCL's env is read once, at ini
 
 // Host kind of a set of operands: 0 = some operand is device memory,
 // 1 = all pinned host memory, 2 = host memory, some of it pageable.
+// Host buffers their owner declared (mi_ccl_comp_register_host_buffer):
+// start -> end.  Each thread searches its own copy, refreshed when the
+// generation moves (a registration or removal), so concurrent workers share
+// nothing but a read-mostly counter; g_host_reg_n lets a process that
+// registers nothing skip it altogether.
+std::mutex g_host_reg_mu;  // writers, and a reader refreshing its copy
+std::map<uintptr_t, uintptr_t> g_host_reg;
+std::atomic<int> g_host_reg_n{0};
+std::atomic<uint64_t> g_host_reg_gen{0};
+thread_local uint64_t t_host_reg_gen = ~0ull;
+thread_local std::vector<std::pair<uintptr_t, uintptr_t>> t_host_reg;
+thread_local unsigned long long t_lookups = 0;
+
+bool registered_host(const void* p, size_t bytes) {
+    if (bytes == 0 || g_host_reg_n.load(std::memory_order_acquire) == 0) return false;
+    if (g_host_reg_gen.load(std::memory_order_acquire) != t_host_reg_gen) {
+        std::lock_guard<std::mutex> lk(g_host_reg_mu);
+        t_host_reg.assign(g_host_reg.begin(), g_host_reg.end());
+        t_host_reg_gen = g_host_reg_gen.load(std::memory_order_relaxed);
+    }
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = std::upper_bound(t_host_reg.begin(), t_host_reg.end(), a,
+                               [](uintptr_t x, const std::pair<uintptr_t, uintptr_t>& r) { return x < r.first; });
+    if (it == t_host_reg.begin()) return false;
+    --it;
+    return a >= it->first && a < it->second && bytes <= it->second - a;
+}
+
+int pointer_kind(const void* p, size_t bytes) {
+    if (registered_host(p, bytes)) return 2;
+    t_lookups++;
+    int dev = -1;
+    return mi_pointer_kind(p, &dev);
+}
+
 // Each distinct pointer is classified once: the lookup
 // (hipPointerGetAttributes) takes a runtime-wide lock, so with several worker
 // threads reducing small host chunks it is the one step that serialises
 // them, and the in-place form passes inout both as out and as the first input.
-int host_kind(const void* const* ptrs, int n, const void* out) {
-    int dev = -1, kind = mi_pointer_kind(out, &dev);
+// `bytes` (0 = unknown) is each operand's extent, for the registry.
+int host_kind(const void* const* ptrs, int n, const void* out, size_t bytes = 0) {
+    int kind = pointer_kind(out, bytes);
     if (kind == 0) return 0;
     for (int i = 0; i < n; i++) {
         if (ptrs[i] == out) continue;
-        const int k = mi_pointer_kind(ptrs[i], &dev);
+        const int k = pointer_kind(ptrs[i], bytes);
         if (k == 0) return 0;
         kind = std::max(kind, k);
     }
     return kind;
 }
 
-bool all_host(const void* const* ptrs, int n, const void* out) { return host_kind(ptrs, n, out) != 0; }
+bool all_host(const void* const* ptrs, int n, const void* out, size_t bytes = 0) {
+    return host_kind(ptrs, n, out, bytes) != 0;
+}
 
 // The dispatcher: host-resident buckets up to the crossover stay on the
 // calling thread's CPU: below it a GPU round trip
@@ -453,7 +492,7 @@ bool all_host(const void* const* ptrs, int n, const void* out) { return host_kin
 bool host_path(const void* const* ins, int k, const void* out, size_t bytes) {
     const HostMax m = mi_host_max();
     if (bytes > std::max(m.pageable, m.pinned)) return false;  // GPU whatever the kinds: skip classifying
-    const int kind = host_kind(ins, k, out);
+    const int kind = host_kind(ins, k, out, bytes);
     if (kind == 0) return false;
     const size_t lim = kind == 1 ? m.pinned : m.pageable;
     return lim > 0 && bytes <= lim;
@@ -653,7 +692,7 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     const HostMax m = mi_host_max();
     // 0: some operand is device memory (or the dispatcher is off), 1: all
     // pinned, 2: host memory, some of it pageable
-    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
+    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out, bytes) : 0;
     const std::vector<int>& devs = shard_devices();
     const HostCall call(kind != 0);  // the thread counts among the host-bucket workers
     if (kind != 0) {
@@ -710,7 +749,7 @@ void settle_split(SplitIssued& sp) {
 int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, int op, unsigned flags,
                mi_request_t* r, SplitIssued* sp = nullptr) {
     const HostMax m = mi_host_max();
-    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out) : 0;
+    const int kind = (m.pageable > 0 || m.pinned > 0) ? host_kind(ins, k, out, count * mi_dtype_size(dt)) : 0;
     if (kind != 0 && shard_devices().size() < 2) {
         const int pk = kind == 1 ? 1 : 0;
         double share = pk ? m.share_pinned : m.share;
@@ -785,7 +824,7 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
     if (!in_buf) MI_CCL_THROW("in_buf is null");
     if (!out_buf) MI_CCL_THROW("out_buf is null");
     const void* src[1] = {in_buf};
-    if (mi_host_max().pageable > 0 && all_host(src, 1, out_buf)) {  // host to host on the CPU, as the reference
+    if (mi_host_max().pageable > 0 && all_host(src, 1, out_buf, bytes)) {  // host to host on the CPU, as the reference
         check(mi_thread_sync(), "mi_thread_sync");
         // (the host path is on only where mi_host_supported(): AVX2 is there)
         check(mi_host_copy(out_buf, in_buf, bytes, use_nontemporal ? 1 : 0), "mi_host_copy");
@@ -1109,6 +1148,42 @@ void ccl_comp_request_free(ccl_comp_request* req) {
     delete req;
     check(rc, "mi_wait");
 }
+
+// The host buffer registry's entry points (include/mi_ccl_comp.h), in both
+// builds: inside oneCCL's tree the schedule's buffer manager calls them.
+extern "C" {
+
+int mi_ccl_comp_register_host_buffer(const void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return (int)MI_E_INVALID;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    if (bytes > UINTPTR_MAX - a) return (int)MI_E_INVALID;
+    try {
+        std::lock_guard<std::mutex> lk(g_host_reg_mu);
+        auto it = g_host_reg.upper_bound(a);  // the first buffer starting after a
+        if (it != g_host_reg.end() && it->first < a + bytes) return (int)MI_E_INVALID;
+        if (it != g_host_reg.begin() && std::prev(it)->second > a) return (int)MI_E_INVALID;
+        g_host_reg.emplace(a, a + bytes);
+        g_host_reg_gen.fetch_add(1, std::memory_order_release);
+    } catch (const std::exception&) {
+        return (int)MI_E_RESOURCE;
+    }
+    g_host_reg_n.fetch_add(1, std::memory_order_release);
+    return 0;
+}
+
+int mi_ccl_comp_unregister_host_buffer(const void* ptr) {
+    std::lock_guard<std::mutex> lk(g_host_reg_mu);
+    auto it = g_host_reg.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_host_reg.end()) return (int)MI_E_INVALID;
+    g_host_reg.erase(it);
+    g_host_reg_gen.fetch_add(1, std::memory_order_release);
+    g_host_reg_n.fetch_sub(1, std::memory_order_release);
+    return 0;
+}
+
+size_t mi_ccl_comp_pointer_lookups(void) { return (size_t)t_lookups; }
+
+}  // extern "C"
 
 #ifndef MI_ONECCL_TREE
 // ===========================================================================

@@ -1,0 +1,159 @@
+"""Host buffer registry of the drop-in (include/mi_ccl_comp.h,
+mi_ccl_comp_register_host_buffer): operands inside a registered buffer skip
+HIP's pointer lookup, which serialises concurrent workers on pageable memory
+(DESIGN.md §6), and the bits stay those of the CPU path.  CPU-only: the
+buffers are host memory below the dispatcher's threshold."""
+import threading
+
+import numpy as np
+import pytest
+
+from oneccl_amd import _lib
+
+MI_E_INVALID = -1
+FLOAT32, SUM = 9, 0
+
+
+@pytest.fixture(scope="module")
+def shim():
+    return _lib.shim()
+
+
+def _reduce(shim, a, b, n=None, off=0):
+    n = len(a) - off if n is None else n
+    rc = shim.mi_ccl_comp_reduce(a.ctypes.data + 4 * off, n, b.ctypes.data + 4 * off, None, FLOAT32, SUM)
+    _lib.check_shim(rc, "ccl_comp_reduce")
+
+
+def test_registered_operands_skip_the_lookup(shim):
+    rng = np.random.default_rng(1)
+    a = rng.random(4096, dtype=np.float32)
+    b0 = rng.random(4096, dtype=np.float32)
+    b = b0.copy()
+    n0 = shim.mi_ccl_comp_pointer_lookups()
+    _reduce(shim, a, b)
+    assert shim.mi_ccl_comp_pointer_lookups() - n0 == 2  # inout once, in once
+    assert shim.mi_ccl_comp_register_host_buffer(a.ctypes.data, a.nbytes) == 0
+    assert shim.mi_ccl_comp_register_host_buffer(b.ctypes.data, b.nbytes) == 0
+    try:
+        b[:] = b0
+        n1 = shim.mi_ccl_comp_pointer_lookups()
+        _reduce(shim, a, b)
+        _reduce(shim, a, b, n=1000, off=3000)  # a chunk inside the registered buffers
+        assert shim.mi_ccl_comp_pointer_lookups() == n1
+        exp = b0 + a
+        exp[3000:4000] += a[3000:4000]
+        assert np.array_equal(b.view(np.uint32), exp.view(np.uint32))
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(a.ctypes.data) == 0
+        assert shim.mi_ccl_comp_unregister_host_buffer(b.ctypes.data) == 0
+    n2 = shim.mi_ccl_comp_pointer_lookups()
+    _reduce(shim, a, b)
+    assert shim.mi_ccl_comp_pointer_lookups() - n2 == 2
+
+
+def test_operand_past_a_registered_buffer_is_looked_up(shim):
+    a = np.ones(2048, dtype=np.float32)
+    b = np.ones(2048, dtype=np.float32)
+    assert shim.mi_ccl_comp_register_host_buffer(a.ctypes.data, 1024 * 4) == 0  # first half only
+    try:
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        _reduce(shim, a, b, n=1024, off=1024)  # wholly outside
+        assert shim.mi_ccl_comp_pointer_lookups() - n0 == 2
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        _reduce(shim, a, b, n=1024, off=512)  # straddles the end
+        assert shim.mi_ccl_comp_pointer_lookups() - n0 == 2
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        _reduce(shim, a, b, n=512, off=0)  # a inside, b not registered
+        assert shim.mi_ccl_comp_pointer_lookups() - n0 == 1
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(a.ctypes.data) == 0
+    exp = np.ones(2048, np.float32)
+    exp[1024:] += 1  # wholly outside
+    exp[512:1536] += 1  # straddling
+    exp[:512] += 1  # a inside
+    assert np.array_equal(b, exp)
+
+
+def test_operand_above_a_registered_buffer_is_looked_up(shim):
+    """An operand past the end of the nearest registered buffer below it is
+    not registered, wherever the two lie (no wrap-around in the range test)."""
+    buf = np.ones(4096, dtype=np.float32)
+    p = buf.ctypes.data
+    assert shim.mi_ccl_comp_register_host_buffer(p, 1024) == 0  # buf[0:256]
+    try:
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        _reduce(shim, buf, buf, n=256, off=2048)  # in place, far above the registered range
+        assert shim.mi_ccl_comp_pointer_lookups() - n0 == 1
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(p) == 0
+    assert np.array_equal(buf[2048:2304], np.full(256, 2, np.float32))
+
+
+def test_registry_rejects_bad_and_overlapping_buffers(shim):
+    a = np.zeros(1024, dtype=np.float32)
+    p = a.ctypes.data
+    assert shim.mi_ccl_comp_register_host_buffer(None, 16) == MI_E_INVALID
+    assert shim.mi_ccl_comp_register_host_buffer(p, 0) == MI_E_INVALID
+    assert shim.mi_ccl_comp_unregister_host_buffer(p) == MI_E_INVALID  # never registered
+    assert shim.mi_ccl_comp_register_host_buffer(p + 1024, 1024) == 0
+    try:
+        assert shim.mi_ccl_comp_register_host_buffer(p, 1025) == MI_E_INVALID  # runs into it
+        assert shim.mi_ccl_comp_register_host_buffer(p + 2047, 16) == MI_E_INVALID  # starts inside it
+        assert shim.mi_ccl_comp_register_host_buffer(p + 1024, 16) == MI_E_INVALID  # same start
+        assert shim.mi_ccl_comp_register_host_buffer(p, 1024) == 0  # adjacent below
+        assert shim.mi_ccl_comp_register_host_buffer(p + 2048, 1024) == 0  # adjacent above
+        assert shim.mi_ccl_comp_unregister_host_buffer(p + 4) == MI_E_INVALID  # not a start
+    finally:
+        for off in (0, 1024, 2048):
+            assert shim.mi_ccl_comp_unregister_host_buffer(p + off) == 0
+
+
+def test_registry_under_concurrent_workers(shim):
+    """Workers reduce inside their registered buffers while another thread
+    registers and unregisters buffers of its own: bits exact, no lookups."""
+    stop = threading.Event()
+    errors = []
+
+    def churn():
+        scratch = [np.zeros(256, np.float32) for _ in range(8)]
+        while not stop.is_set():
+            for s in scratch:
+                if shim.mi_ccl_comp_register_host_buffer(s.ctypes.data, s.nbytes) != 0:
+                    errors.append("register")
+            for s in scratch:
+                if shim.mi_ccl_comp_unregister_host_buffer(s.ctypes.data) != 0:
+                    errors.append("unregister")
+
+    def worker(seed):
+        rng = np.random.default_rng(seed)
+        a = rng.random(8192, dtype=np.float32)
+        b0 = rng.random(8192, dtype=np.float32)
+        b = b0.copy()
+        shim.mi_ccl_comp_register_host_buffer(a.ctypes.data, a.nbytes)
+        shim.mi_ccl_comp_register_host_buffer(b.ctypes.data, b.nbytes)
+        try:
+            n0 = shim.mi_ccl_comp_pointer_lookups()
+            exp = b0.copy()
+            for i in range(200):
+                off = (i * 97) % 4096
+                _reduce(shim, a, b, n=4096, off=off)
+                exp[off:off + 4096] += a[off:off + 4096]
+            if shim.mi_ccl_comp_pointer_lookups() != n0:
+                errors.append("lookup")
+            if not np.array_equal(b.view(np.uint32), exp.view(np.uint32)):
+                errors.append("bits")
+        finally:
+            shim.mi_ccl_comp_unregister_host_buffer(a.ctypes.data)
+            shim.mi_ccl_comp_unregister_host_buffer(b.ctypes.data)
+
+    ch = threading.Thread(target=churn)
+    ch.start()
+    ws = [threading.Thread(target=worker, args=(s,)) for s in range(4)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    stop.set()
+    ch.join()
+    assert errors == []

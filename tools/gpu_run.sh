@@ -87,7 +87,10 @@ for step in "$@"; do
             run xcd 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 8 xcd ;;
         ptrkind)  # pointer classification and small host reduces against concurrent threads
             run ptrkind 300 ./tools/pointer_kind_probe &&
-            for T in 1 2 4 8 16; do run "small_workers_$T" 120 ./tools/small_workers $T 1024; done ;;
+            for T in 1 2 4 8 16; do
+                run "small_workers_$T" 120 ./tools/small_workers $T 1024 &&
+                run "small_workers_reg_$T" 120 ./tools/small_workers $T 1024 reg
+            done ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)
