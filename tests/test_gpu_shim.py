@@ -871,3 +871,28 @@ def test_process_exit_with_unwaited_async_requests():
                        env=env)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "exit-async: ok" in r.stdout
+
+
+@pytest.mark.parametrize("n", [4099, (40 << 20) // 4 + 33])
+@pytest.mark.parametrize("dt", [FP32, BF16])
+def test_registered_pageable_on_gpu_paths(n, dt):
+    """Pageable operands inside registered host buffers
+    (mi_ccl_comp_register_host_buffer) take the GPU paths — bounce buffers for
+    small buckets, the staged pipeline past one chunk — with the oracle's bits
+    and without HIP's pointer lookup."""
+    shim = _lib.shim()
+    b_impl, f_impl = impls()
+    a = rand_array(dt, n, seed=91, specials=False)
+    b = rand_array(dt, n, seed=92, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+    assert shim.mi_ccl_comp_register_host_buffer(ptr(a), a.nbytes) == 0
+    assert shim.mi_ccl_comp_register_host_buffer(ptr(b), b.nbytes) == 0
+    try:
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        comp.comp_reduce(ptr(a), n, ptr(b), comp.datatype(dt), comp.reduction.sum)
+        assert shim.mi_ccl_comp_pointer_lookups() == n0
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(ptr(a)) == 0
+        assert shim.mi_ccl_comp_unregister_host_buffer(ptr(b)) == 0
+    assert_same(b, exp, dt)
