@@ -27,7 +27,8 @@ extern "C" {
 typedef void (*mi_ccl_reduction_fn)(const void* in_buf, size_t in_count, void* inout_buf,
                                     size_t* out_count, int dtype, const void* context);
 
-/* ccl_comp_reduce(nullptr sched, ...), src/comp/comp.cpp:123-200 */
+/* ccl_comp_reduce(sched, ...), src/comp/comp.cpp:123-200; sched = none
+ * unless mi_ccl_comp_shim_sched chose one for the calling thread */
 int mi_ccl_comp_reduce(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
                        int dtype, int op);
 /* ccl_comp_reduce with ccl::reduction::custom and a user callback,
@@ -102,18 +103,27 @@ int mi_ccl_comp_split_take_gpu_alone(int pinned);
 int mi_ccl_comp_split_feed(int pinned, size_t count, size_t head, double t_head, double t_tail);
 /* The dispatcher's thresholds and default shares in force (after env).     */
 int mi_ccl_comp_host_max(size_t* pageable, size_t* pinned, double* share, double* share_pinned);
-/* Host buffer registry.  A caller that owns host memory (oneCCL's schedule
- * buffers: sched->alloc_buffer, src/sched/buffer/buffer_manager.cpp) may
- * declare [ptr, ptr + bytes) as host memory until it unregisters it; an
- * operand lying wholly inside a registered buffer is taken as pageable host
- * memory without asking HIP, whose lookup of pageable pointers serialises
- * concurrent workers.  Registered memory must not be device
- * memory; pinned memory registered here is treated as pageable (staged, not
- * read in place).  Buffers may not overlap.  0 or an MI_E_* code.          */
+/* Host buffer registry.  A caller that owns long-lived host memory
+ * (oneCCL's regular_buffer_cache, src/sched/buffer/buffer_cache.cpp:87-123;
+ * integration/0005) declares [ptr, ptr + bytes) until it unregisters it
+ * (by the start address, before freeing).  An operand lying wholly inside a
+ * registered buffer is classified without asking HIP, whose lookup of
+ * pageable pointers serialises concurrent workers -- by the
+ * dispatcher and by libmi_reduce's GPU path alike (mi_host_declare).  The
+ * range is looked up once, here: device or managed memory is refused with
+ * MI_E_INVALID, pinned memory keeps its zero-copy path.  Buffers may not
+ * overlap.  0 or an MI_E_* code.                                           */
 int mi_ccl_comp_register_host_buffer(const void* ptr, size_t bytes);
 int mi_ccl_comp_unregister_host_buffer(const void* ptr);
-/* Pointer lookups through HIP made by the calling thread so far.  Diagnostic. */
+/* HIP pointer lookups made by the calling thread so far, in this shim and in
+ * libmi_reduce (mi_pointer_lookups).  Diagnostic.                          */
 size_t mi_ccl_comp_pointer_lookups(void);
+/* Test hook: the schedule this thread's C-view calls pass to
+ * ccl_comp_reduce / _start: 0 = none (nullptr, the default), 1 = a schedule
+ * whose collective has no stream (operands are host memory by its word and
+ * are not looked up, comp.cpp:136-142), 2 = one with a stream (looked up).
+ * Returns the previous mode, or MI_E_INVALID.                              */
+int mi_ccl_comp_shim_sched(int mode);
 /* The impl types in force: ccl_bf16_impl_type / ccl_fp16_impl_type values. */
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl);
 const char* mi_ccl_last_error(void);

@@ -35,9 +35,13 @@
 struct ccl_comp_request;  // opaque; one per started reduce
 
 /* Issue inout_buf = op(in_buf, inout_buf) and return at once; *req receives
- * the request to poll.  Always returns ccl::status::success (errors throw). */
-ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf,
-                                  size_t* out_count, const ccl_datatype& dtype,
+ * the request to poll.  Always returns ccl::status::success (errors throw).
+ * `sched` is the calling entry's schedule, as for ccl_comp_reduce: when its
+ * collective has no stream (sched->coll_param.stream == nullptr) the
+ * operands are host memory and are not looked up (the reference's
+ * comp.cpp:136-142); nullptr = no schedule, operands looked up.           */
+ccl::status ccl_comp_reduce_start(ccl_sched* sched, const void* in_buf, size_t in_count,
+                                  void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
                                   ccl::reduction reduction, ccl::reduction_fn reduction_fn,
                                   const ccl::fn_context* context, ccl_comp_request** req);
 
@@ -45,7 +49,8 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
  * K-input fold of in_buf + offsets[i] * dtype.size() into inout_buf, as one
  * request (several chained launches past 16 inputs).  The fp32 scratch
  * `tmp` / `acc` of the synchronous form is not needed and not taken.     */
-ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<size_t>& offsets,
+ccl::status ccl_comp_batch_reduce_start(ccl_sched* sched, const void* in_buf,
+                                        const std::vector<size_t>& offsets,
                                         size_t in_count, void* inout_buf, size_t* out_count,
                                         const ccl_datatype& dtype, ccl::reduction reduction,
                                         ccl::reduction_fn reduction_fn,

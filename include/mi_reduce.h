@@ -272,6 +272,33 @@ int mi_shard_range(size_t count, int rank, int world, size_t align,
  * memory; 2 = pageable host memory.  What ccl_comp_reduce's SYCL branch asks
  * sycl::get_pointer_type for (src/comp/comp.cpp:145-147).                 */
 int mi_pointer_kind(const void* ptr, int* device);
+/* The same for the operand [ptr, ptr + bytes): answered from the declared
+ * host ranges below when it lies wholly inside one, else by HIP.          */
+int mi_pointer_kind_range(const void* ptr, size_t bytes, int* device);
+
+/* ---- declared host ranges --------------------------------------------- *
+ * HIP's pointer lookup serialises concurrent callers on pageable memory
+ * (0.07 us alone, 9.5 us per call at 16 threads on MI355X).
+ * A caller that owns long-lived host buffers declares them once: every
+ * entry point then classifies an operand lying wholly inside a declared
+ * range without asking HIP (readers take no lock).  mi_host_declare looks
+ * the range up once (both ends): device or managed memory is refused with
+ * MI_E_INVALID, as is a range mixing kinds; pinned ranges stay pinned (the
+ * zero-copy path), pageable ones pageable.  Declare after any
+ * mi_host_register of the same buffer.  Ranges may not overlap.  Undeclare
+ * (by the start address) before the memory is freed; a range must not be
+ * undeclared while a reduce on it is in flight.  oneCCL's
+ * regular_buffer_cache declares its buffers (integration/0005, INTEGRATION.md
+ * §2f; the place it registers them with Level Zero,
+ * src/sched/buffer/buffer_cache.cpp:99-104).                               */
+int mi_host_declare(const void* ptr, size_t bytes);
+int mi_host_undeclare(const void* ptr);
+/* Kind (1 pinned, 2 pageable) of a declared range holding the operand, or
+ * -1 when none does.  No HIP call.  Diagnostic.                           */
+int mi_host_declared_kind(const void* ptr, size_t bytes);
+/* HIP pointer lookups made by the calling thread so far (every entry point's
+ * classification, declared ranges excepted).  Diagnostic.                  */
+size_t mi_pointer_lookups(void);
 
 /* ---- staging-buffer registration ------------------------------------- *
  * Pin (page-lock and map for every GPU) an existing pageable host buffer, so
@@ -343,6 +370,11 @@ int mi_set_max_blocks(int max_blocks);
  * a worker oneCCL pinned to one core do not share that core.  0 = helpers
  * inherit their creator's mask (MI_REDUCE_HELPER_AFFINITY=inherit).       */
 int mi_helper_cpu_count(void);
+/* Test hook: a library thread holds an exit guard (the section the exit
+ * handler waits for) for hold_ms milliseconds, < 0 = forever.  The handler
+ * waits at most MI_REDUCE_EXIT_WAIT_S seconds (default 60), then names the
+ * section on stderr and ends the process with status 70.                  */
+int mi_test_hold_exit_guard(int hold_ms);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,8 @@ public:
             (*std::max_element(offsets.begin(), offsets.end()) + cnt) * dtype.size();
         const ccl::fn_context context = { sched->coll_attr.match_id.c_str(),
                                           inout_buf.get_offset() };
-        ccl_comp_batch_reduce_start(in_buf.get_ptr(in_bytes),
+        ccl_comp_batch_reduce_start(sched, /* host memory unless its collective has a stream */
+                                    in_buf.get_ptr(in_bytes),
                                     offsets,
                                     cnt,
                                     inout_buf.get_ptr(bytes),

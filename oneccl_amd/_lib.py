@@ -65,6 +65,12 @@ MI_API = [
     ("mi_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("mi_shard_range", c_int, [c_size_t, c_int, c_int, c_size_t, POINTER(c_size_t), POINTER(c_size_t)]),
     ("mi_pointer_kind", c_int, [c_void_p, POINTER(c_int)]),
+    ("mi_pointer_kind_range", c_int, [c_void_p, c_size_t, POINTER(c_int)]),
+    ("mi_host_declare", c_int, [c_void_p, c_size_t]),
+    ("mi_host_undeclare", c_int, [c_void_p]),
+    ("mi_host_declared_kind", c_int, [c_void_p, c_size_t]),
+    ("mi_pointer_lookups", c_size_t, []),
+    ("mi_test_hold_exit_guard", c_int, [c_int]),
     ("mi_host_register", c_int, [c_void_p, c_size_t]),
     ("mi_host_unregister", c_int, [c_void_p]),
     ("mi_reduction_to_str", c_char_p, [c_int]),
@@ -115,6 +121,7 @@ SHIM_API = [
     ("mi_ccl_comp_register_host_buffer", c_int, [c_void_p, c_size_t]),
     ("mi_ccl_comp_unregister_host_buffer", c_int, [c_void_p]),
     ("mi_ccl_comp_pointer_lookups", c_size_t, []),
+    ("mi_ccl_comp_shim_sched", c_int, [c_int]),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
     ("mi_ccl_last_error", c_char_p, []),
 ]

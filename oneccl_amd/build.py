@@ -166,7 +166,7 @@ def build_small_workers(force: bool = False) -> Path:
     src = ROOT / "tools" / "small_workers.cpp"
     if src.exists() and (force or _stale(out, [src, LIB / "libccl_comp_hip.so"])):
         _run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'include'}", "-o", str(out), str(src), f"-L{LIB}",
-              "-lccl_comp_hip", "-Wl,-rpath,$ORIGIN/../oneccl_amd/lib", "-pthread"])
+              "-lccl_comp_hip", "-Wl,-rpath,$ORIGIN/../oneccl_amd/lib", "-pthread", "-ldl"])
     return out
 
 

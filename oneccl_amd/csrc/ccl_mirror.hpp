@@ -72,7 +72,19 @@ enum status : int {
 
 }  // namespace ccl
 
-class ccl_sched;  // opaque here: src/comp only reads it on the SYCL branch
+// The one thing src/comp reads of a schedule: its collective's stream
+// (sched->coll_param.stream, src/sched/sched_base.hpp:151,
+// src/coll/coll_param.hpp:129; the reference's comp.cpp:137).  The
+// standalone ccl_sched carries only that; the mangled names depend on the
+// class name alone.
+class ccl_stream;  // opaque
+struct ccl_coll_param {
+    ccl_stream* stream = nullptr;
+};
+class ccl_sched {
+public:
+    ccl_coll_param coll_param;
+};
 
 class ccl_datatype {
 public:

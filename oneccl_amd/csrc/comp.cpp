@@ -44,9 +44,14 @@
 #include "comp/bf16/bf16.hpp"
 #include "comp/comp.hpp"
 #include "comp/fp16/fp16.hpp"
+#include "sched/sched.hpp"  // sched->coll_param.stream, as the reference's comp.cpp reads it
 #define MI_CCL_THROW(msg) CCL_THROW(msg)
 #define MI_CCL_FATAL(msg) CCL_FATAL(msg)
-#include "mi_ccl_comp_async.hpp"  // include/ (on the include path)
+// the dispatcher's decisions go to oneCCL's own log (CCL_LOG_LEVEL=debug),
+// as the reference logs its path (bf16.cpp:92, fp16.cpp:46, comp.cpp:149)
+#define MI_LOG_DEBUG(...) LOG_DEBUG(__VA_ARGS__)
+#include "mi_ccl_comp.h"  // include/ (on the include path)
+#include "mi_ccl_comp_async.hpp"
 static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
 static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
 // CCL_COMP_HIP_DEVICE: the GPU for operands that name none (host buffers);
@@ -61,9 +66,28 @@ static int mi_comp_device() {
 struct HostMax;
 static HostMax mi_host_max();
 #else
+#include <sstream>
+
 #include "../../include/mi_ccl_comp.h"
 #include "ccl_mirror.hpp"
 #define MI_CCL_THROW(msg) throw ccl::exception(msg)
+// oneCCL's LOG_DEBUG (src/common/log/log.hpp:302-314) for the standalone
+// build: CCL_LOG_LEVEL=debug (or trace) prints the dispatcher's decisions to
+// stderr in oneCCL's format; the arguments are only evaluated when it is on.
+static bool mi_log_debug_on();
+template <typename... A>
+static void mi_log_debug(int line, const char* fn, const A&... a) {
+    std::ostringstream os;
+    os << "|CCL_DEBUG| comp.cpp:" << line << " " << fn << ": ";
+    using expand = int[];
+    (void)expand{0, ((void)(os << a), 0)...};
+    os << "\n";
+    fputs(os.str().c_str(), stderr);
+}
+#define MI_LOG_DEBUG(...)                                                   \
+    do {                                                                    \
+        if (mi_log_debug_on()) mi_log_debug(__LINE__, __FUNCTION__, __VA_ARGS__); \
+    } while (0)
 // CCL_FATAL (src/common/log/log.hpp:333-337): log the error, std::terminate().
 // The reference uses it for an unknown dtype or reduction (comp.cpp:56,113,
 // bf16.cpp:73, bf16_intrisics.hpp:131, fp16_intrisics.hpp:222-243); the
@@ -179,6 +203,7 @@ struct MiEnv {
     ccl_fp16_impl_type fp16 = ccl_fp16_no_compiler_support;
     int device = -1;  // CCL_COMP_HIP_DEVICE
     HostMax host_max;  // CCL_COMP_HOST_MAX_BYTES, CCL_COMP_HOST_MAX_PINNED_BYTES
+    bool log_debug = false;  // CCL_LOG_LEVEL=debug|trace (env.cpp's log level)
 };
 
 // The parsed environment is an immutable snapshot published through an
@@ -253,6 +278,7 @@ void parse_env_locked() {
         MI_CCL_THROW("unsupported FP16 impl type: " + fp16_impl_names[e.fp16]);
     if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) e.device = atoi(v);
     e.host_max = parse_host_max();
+    if (const char* v = getenv("CCL_LOG_LEVEL")) e.log_debug = !strcmp(v, "debug") || !strcmp(v, "trace");
     g_env_all.push_back(std::move(snap));
     g_env_cur.store(g_env_all.back().get(), std::memory_order_release);
 }
@@ -270,6 +296,7 @@ static ccl_bf16_impl_type mi_bf16_impl() { return env().bf16; }
 static ccl_fp16_impl_type mi_fp16_impl() { return env().fp16; }
 static int mi_comp_device() { return env().device; }
 static HostMax mi_host_max() { return env().host_max; }
+static bool mi_log_debug_on() { return env().log_debug; }
 #endif  // !MI_ONECCL_TREE
 
 // ---------------------------------------------------------------------------
@@ -324,6 +351,25 @@ void check(int rc, const char* where) {
     if (rc != 0) MI_CCL_THROW(std::string(where) + " failed: " + mi_last_error());
 }
 
+// The schedule's word on where the operands live, as the reference takes it
+// (src/comp/comp.cpp:136-142): a schedule whose collective has no stream
+// (sched->coll_param.stream, src/coll/coll_param.hpp:129) works on host
+// memory only -- the reference then calls ccl_comp_reduce_regular on the CPU
+// without classifying anything, and a build without SYCL never classifies
+// (:196-198).  With a stream, or with no schedule (the MPI user op,
+// atl_mpi_ctx.cpp:87-124, and this repo's C view), the operands are looked
+// up.  The word holds for the duration of one entry-point call on this
+// thread (SchedScope).
+thread_local bool t_host_by_sched = false;
+
+bool host_schedule(const ccl_sched* sched) { return sched && !sched->coll_param.stream; }
+
+struct SchedScope {
+    const bool prev;
+    explicit SchedScope(const ccl_sched* sched) : prev(t_host_by_sched) { t_host_by_sched = host_schedule(sched); }
+    ~SchedScope() { t_host_by_sched = prev; }
+};
+
 bool is_device_ptr(const void* p) {
     int dev = -1;
     return mi_pointer_kind(p, &dev) == 0;
@@ -335,7 +381,9 @@ bool is_device_ptr(const void* p) {
 void run_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
                 const ccl_datatype& dtype, ccl::reduction_fn fn, const ccl::fn_context* context) {
     if (!fn) MI_CCL_THROW("custom reduction requires user callback");
-    const bool din = is_device_ptr(in_buf), dio = is_device_ptr(inout_buf);
+    // host memory by the schedule's word: straight to the callback, as the
+    // reference does (comp.cpp:139-142)
+    const bool din = !t_host_by_sched && is_device_ptr(in_buf), dio = !t_host_by_sched && is_device_ptr(inout_buf);
     if (!din && !dio) {
         fn(in_buf, in_count, inout_buf, out_count, dtype.idx(), context);
         return;
@@ -429,41 +477,18 @@ void shard_env_reload() {  // standalone only: oneCCL's env is read once, at ini
 #endif
 
 // Host kind of a set of operands: 0 = some operand is device memory,
-// 1 = all pinned host memory, 2 = host memory, some of it pageable.
-// Host buffers their owner declared (mi_ccl_comp_register_host_buffer):
-// start -> end.  Each thread searches its own copy, refreshed when the
-// generation moves (a registration or removal), so concurrent workers share
-// nothing but a read-mostly counter; g_host_reg_n lets a process that
-// registers nothing skip it altogether.
-std::mutex g_host_reg_mu;  // writers, and a reader refreshing its copy
-std::map<uintptr_t, uintptr_t> g_host_reg;
-std::atomic<int> g_host_reg_n{0};
-std::atomic<uint64_t> g_host_reg_gen{0};
-thread_local uint64_t t_host_reg_gen = ~0ull;
-thread_local std::vector<std::pair<uintptr_t, uintptr_t>> t_host_reg;
-thread_local unsigned long long t_lookups = 0;
-
-bool registered_host(const void* p, size_t bytes) {
-    if (bytes == 0 || g_host_reg_n.load(std::memory_order_acquire) == 0) return false;
-    if (g_host_reg_gen.load(std::memory_order_acquire) != t_host_reg_gen) {
-        std::lock_guard<std::mutex> lk(g_host_reg_mu);
-        t_host_reg.assign(g_host_reg.begin(), g_host_reg.end());
-        t_host_reg_gen = g_host_reg_gen.load(std::memory_order_relaxed);
-    }
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto it = std::upper_bound(t_host_reg.begin(), t_host_reg.end(), a,
-                               [](uintptr_t x, const std::pair<uintptr_t, uintptr_t>& r) { return x < r.first; });
-    if (it == t_host_reg.begin()) return false;
-    --it;
-    return a >= it->first && a < it->second && bytes <= it->second - a;
-}
+// 1 = all pinned host memory, 2 = host memory, some of it pageable,
+// 3 = host memory by the schedule's word (kHostBySched, below: not looked up,
+// routed as 2).  Each lookup goes to libmi_reduce (mi_pointer_kind_range),
+// which answers from the host ranges their owner declared
+// (mi_ccl_comp_register_host_buffer -> mi_host_declare) without asking HIP.
+constexpr int kHostBySched = 3;
 
 int pointer_kind(const void* p, size_t bytes) {
-    if (registered_host(p, bytes)) return 2;
-    t_lookups++;
     int dev = -1;
-    return mi_pointer_kind(p, &dev);
+    return mi_pointer_kind_range(p, bytes, &dev);
 }
+
 
 // Each distinct pointer is classified once: the lookup
 // (hipPointerGetAttributes) takes a runtime-wide lock, so with several worker
@@ -471,6 +496,13 @@ int pointer_kind(const void* p, size_t bytes) {
 // them, and the in-place form passes inout both as out and as the first input.
 // `bytes` (0 = unknown) is each operand's extent, for the registry.
 int host_kind(const void* const* ptrs, int n, const void* out, size_t bytes = 0) {
+    if (t_host_by_sched) {
+        // host memory by the schedule's word: a bucket that takes the CPU
+        // path whatever its pointer kinds needs no lookup at all; above
+        // that the kinds still pick pinned zero-copy or staging
+        const HostMax m = mi_host_max();
+        if (m.pageable > 0 && m.pinned > 0 && bytes <= std::min(m.pageable, m.pinned)) return kHostBySched;
+    }
     int kind = pointer_kind(out, bytes);
     if (kind == 0) return 0;
     for (int i = 0; i < n; i++) {
@@ -486,13 +518,35 @@ bool all_host(const void* const* ptrs, int n, const void* out, size_t bytes = 0)
     return host_kind(ptrs, n, out, bytes) != 0;
 }
 
+// ---- the dispatcher's decision, logged ------------------------------------
+const char* kind_name(int kind) {
+    switch (kind) {
+        case 0: return "device memory (or not classified: dispatcher off)";
+        case 1: return "pinned host memory";
+        case 2: return "host memory, some pageable";
+        default: return "host memory by the schedule (no stream; not looked up)";
+    }
+}
+
+// the GPU's route for operands of this kind (mi_reduce.hip reduce_issue)
+const char* gpu_route(int kind) {
+    return kind == 0 ? "gpu" : kind == 1 ? "gpu zero-copy (pinned, read in place)" : "gpu staged (pageable)";
+}
+
+void log_route(const char* what, size_t count, int dt, int k, int kind, const char* path, double share = -1.0) {
+    MI_LOG_DEBUG(what, ": count ", count, ", dtype ", dt, ", bytes ", count * mi_dtype_size(dt), ", inputs ", k,
+                 ", operands: ", kind_name(kind), ", path: ", path,
+                 share >= 0 ? ", cpu head share " : "", share >= 0 ? std::to_string(share) : std::string());
+}
+
 // The dispatcher: host-resident buckets up to the crossover stay on the
 // calling thread's CPU: below it a GPU round trip
 // costs more than the reduce.
-bool host_path(const void* const* ins, int k, const void* out, size_t bytes) {
+bool host_path(const void* const* ins, int k, const void* out, size_t bytes, int* kind_out = nullptr) {
     const HostMax m = mi_host_max();
     if (bytes > std::max(m.pageable, m.pinned)) return false;  // GPU whatever the kinds: skip classifying
     const int kind = host_kind(ins, k, out, bytes);
+    if (kind_out) *kind_out = kind;
     if (kind == 0) return false;
     const size_t lim = kind == 1 ? m.pinned : m.pageable;
     return lim > 0 && bytes <= lim;
@@ -601,6 +655,8 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
         if (cur < 0) cur = share;
         share = cur;
         if (take_gpu_alone(pk)) {  // the GPU alone, timed
+            log_route("reduce", count, dt, k, pinned ? 1 : 2, pinned ? "gpu zero-copy alone (timed against the split)"
+                                                                     : "gpu staged alone (timed against the split)");
             const double t0 = now_s();
             const int rc = mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
             if (rc == 0) gpu_alone_timed(pk, count, now_s() - t0);
@@ -610,7 +666,11 @@ int coop_fold(const void* const* ins, int k, void* out, size_t count, int dt, in
     const size_t es = mi_dtype_size(dt);
     size_t s = (size_t)((double)count * share);
     s -= s % 256;
-    if (s == 0 || s >= count) return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+    if (s == 0 || s >= count) {
+        log_route("reduce", count, dt, k, pinned ? 1 : 2, gpu_route(pinned ? 1 : 2));
+        return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
+    }
+    log_route("reduce", count, dt, k, pinned ? 1 : 2, "split: calling thread's cpu head + gpu tail", share);
     if (int rc = mi_thread_sync()) return rc;  // earlier requests of this thread first
     const void* gins[MI_MAX_INPUTS];
     for (int i = 0; i < k; i++) gins[i] = static_cast<const char*>(ins[i]) + s * es;
@@ -697,11 +757,17 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     const HostCall call(kind != 0);  // the thread counts among the host-bucket workers
     if (kind != 0) {
         const size_t lim = kind == 1 ? m.pinned : m.pageable;
-        if (lim > 0 && bytes <= lim) return host_fold(ins, k, out, count, dt, op, flags);
+        if (lim > 0 && bytes <= lim) {
+            log_route("reduce", count, dt, k, kind, "cpu (calling thread)");
+            return host_fold(ins, k, out, count, dt, op, flags);
+        }
         const double share = kind == 1 ? m.share_pinned : m.share;
         if (devs.size() < 2 && share > 0) {
             const int limit = kind == 1 ? m.split_workers_pinned : m.split_workers;
-            if (limit > 0 && host_workers() > limit) return host_fold(ins, k, out, count, dt, op, flags);
+            if (limit > 0 && host_workers() > limit) {
+                log_route("reduce", count, dt, k, kind, "cpu (calling thread; more host workers than the split cap)");
+                return host_fold(ins, k, out, count, dt, op, flags);
+            }
             return coop_fold(ins, k, out, count, dt, op, flags, share, kind == 1,
                              kind == 1 ? m.adapt_pinned : m.adapt);
         }
@@ -709,9 +775,12 @@ int fold_sync(const void* const* ins, int k, void* out, size_t count, int dt, in
     if (devs.size() >= 2) {
         bool host = !is_device_ptr(out);
         for (int i = 0; i < k && host; i++) host = !is_device_ptr(ins[i]);
-        if (host)
+        if (host) {
+            log_route("reduce", count, dt, k, kind == 0 ? 2 : kind, "gpu sharded over CCL_COMP_HIP_SHARD_DEVICES");
             return mi_reduce_multi_sync_sharded(ins, k, out, count, dt, op, flags, (int)devs.size(), devs.data());
+        }
     }
+    log_route("reduce", count, dt, k, kind, gpu_route(kind));
     return mi_reduce_multi_sync(ins, k, out, count, dt, op, flags, mi_comp_device());
 }
 
@@ -760,6 +829,8 @@ int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, i
         }
         const int limit = pk ? m.split_workers_pinned : m.split_workers;
         if (adapt && sp && !sp->req && take_gpu_alone(pk)) {  // the GPU alone, timed where it runs
+            log_route("reduce_start", count, dt, k, kind, pk ? "gpu zero-copy alone (timed against the split)"
+                                                             : "gpu staged alone (timed against the split)");
             const int rc = mi_reduce_start_timed(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
             if (rc == 0) {
                 sp->req = *r;
@@ -773,6 +844,8 @@ int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, i
             size_t s = (size_t)((double)count * share);
             s -= s % 256;
             if (s > 0 && s < count) {
+                log_route("reduce_start", count, dt, k, kind, "split: staging worker's cpu head + gpu tail",
+                          (double)s / (double)count);
                 const int rc =
                     mi_reduce_split_start(ins, k, out, count, dt, op, flags, mi_comp_device(), s, &mi_host_reduce, r);
                 if (rc == 0 && adapt && sp && !sp->req) {
@@ -785,6 +858,7 @@ int start_fold(const void* const* ins, int k, void* out, size_t count, int dt, i
             }
         }
     }
+    log_route("reduce_start", count, dt, k, kind, gpu_route(kind));
     return mi_reduce_start(ins, k, out, count, dt, op, flags, mi_comp_device(), r);
 }
 
@@ -918,10 +992,11 @@ ccl::status ccl_comp_reduce_regular(const void* in_buf, size_t in_count, void* i
     return ccl::status::success;
 }
 
-ccl::status ccl_comp_reduce(ccl_sched* /*sched*/, const void* in_buf, size_t in_count, void* inout_buf,
+ccl::status ccl_comp_reduce(ccl_sched* sched, const void* in_buf, size_t in_count, void* inout_buf,
                             size_t* out_count, const ccl_datatype& dtype, ccl::reduction reduction,
                             ccl::reduction_fn reduction_fn, const ccl::fn_context* context) {
     if (!in_count) return ccl::status::success;
+    const SchedScope scope(sched);  // comp.cpp:136-142: no stream -> host memory, nothing looked up
     return ccl_comp_reduce_regular(in_buf, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context);
 }
 
@@ -1043,11 +1118,13 @@ struct ccl_comp_request {
     SplitIssued split;            // the first adaptive split among them, if any
 };
 
-ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count,
-                                  const ccl_datatype& dtype, ccl::reduction reduction, ccl::reduction_fn reduction_fn,
-                                  const ccl::fn_context* context, ccl_comp_request** req) {
+ccl::status ccl_comp_reduce_start(ccl_sched* sched, const void* in_buf, size_t in_count, void* inout_buf,
+                                  size_t* out_count, const ccl_datatype& dtype, ccl::reduction reduction,
+                                  ccl::reduction_fn reduction_fn, const ccl::fn_context* context,
+                                  ccl_comp_request** req) {
     if (!req) MI_CCL_THROW("null request pointer");
     *req = nullptr;
+    const SchedScope scope(sched);
     std::unique_ptr<ccl_comp_request> q(new ccl_comp_request());
     if (in_count) {  // comp.cpp:132-134
         if (reduction == ccl::reduction::custom) {
@@ -1066,7 +1143,9 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
             unsigned f = 0;
             if (reduce_semantics(dt, &f)) {
                 const void* ins[2] = {inout_buf, in_buf};
-                if (host_path(ins, 2, inout_buf, in_count * mi_dtype_size(dt))) {  // completes here
+                int kind = 0;
+                if (host_path(ins, 2, inout_buf, in_count * mi_dtype_size(dt), &kind)) {  // completes here
+                    log_route("reduce_start", in_count, dt, 2, kind, "cpu (calling thread; completes in start)");
                     check(host_fold(ins, 2, inout_buf, in_count, dt, static_cast<int>(reduction), f), "host reduce");
                     *req = q.release();
                     return ccl::status::success;
@@ -1082,13 +1161,14 @@ ccl::status ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* ino
     return ccl::status::success;
 }
 
-ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<size_t>& offsets, size_t in_count,
-                                        void* inout_buf, size_t* out_count, const ccl_datatype& dtype,
-                                        ccl::reduction reduction, ccl::reduction_fn reduction_fn,
-                                        const ccl::fn_context* context, int bf16_keep_precision_mode,
-                                        ccl_comp_request** req) {
+ccl::status ccl_comp_batch_reduce_start(ccl_sched* sched, const void* in_buf, const std::vector<size_t>& offsets,
+                                        size_t in_count, void* inout_buf, size_t* out_count,
+                                        const ccl_datatype& dtype, ccl::reduction reduction,
+                                        ccl::reduction_fn reduction_fn, const ccl::fn_context* context,
+                                        int bf16_keep_precision_mode, ccl_comp_request** req) {
     if (!req) MI_CCL_THROW("null request pointer");
     *req = nullptr;
+    const SchedScope scope(sched);
     std::unique_ptr<ccl_comp_request> q(new ccl_comp_request());
     struct Drop {  // on a throw, wait for and release what was already issued
         ccl_comp_request* q;
@@ -1105,7 +1185,10 @@ ccl::status ccl_comp_batch_reduce_start(const void* in_buf, const std::vector<si
     batch_reduce_body(in_buf, offsets, in_count, inout_buf, out_count, dtype, reduction, reduction_fn, context,
                       bf16_keep_precision_mode, nullptr, nullptr,
                       [&](const void* const* ins, int k, void* out, size_t n, int dt, int op, unsigned f) {
-                          if (host_path(ins, k, out, n * mi_dtype_size(dt))) {  // small host bucket: done here
+                          int kind = 0;
+                          if (host_path(ins, k, out, n * mi_dtype_size(dt), &kind)) {  // small host bucket: done here
+                              log_route("batch_reduce_start", n, dt, k, kind,
+                                        "cpu (calling thread; completes in start)");
                               check(host_fold(ins, k, out, n, dt, op, f), "host reduce");
                               return;
                           }
@@ -1150,38 +1233,18 @@ void ccl_comp_request_free(ccl_comp_request* req) {
 }
 
 // The host buffer registry's entry points (include/mi_ccl_comp.h), in both
-// builds: inside oneCCL's tree the schedule's buffer manager calls them.
+// builds: inside oneCCL's tree the regular buffer cache calls them
+// (integration/0005).  The ranges live in libmi_reduce (mi_host_declare), so
+// every classification -- the dispatcher's here and the GPU path's there --
+// answers from them without asking HIP; a range is looked up once, when
+// declared: device memory is refused, pinned memory stays pinned.
 extern "C" {
 
-int mi_ccl_comp_register_host_buffer(const void* ptr, size_t bytes) {
-    if (!ptr || bytes == 0) return (int)MI_E_INVALID;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
-    if (bytes > UINTPTR_MAX - a) return (int)MI_E_INVALID;
-    try {
-        std::lock_guard<std::mutex> lk(g_host_reg_mu);
-        auto it = g_host_reg.upper_bound(a);  // the first buffer starting after a
-        if (it != g_host_reg.end() && it->first < a + bytes) return (int)MI_E_INVALID;
-        if (it != g_host_reg.begin() && std::prev(it)->second > a) return (int)MI_E_INVALID;
-        g_host_reg.emplace(a, a + bytes);
-        g_host_reg_gen.fetch_add(1, std::memory_order_release);
-    } catch (const std::exception&) {
-        return (int)MI_E_RESOURCE;
-    }
-    g_host_reg_n.fetch_add(1, std::memory_order_release);
-    return 0;
-}
+int mi_ccl_comp_register_host_buffer(const void* ptr, size_t bytes) { return mi_host_declare(ptr, bytes); }
 
-int mi_ccl_comp_unregister_host_buffer(const void* ptr) {
-    std::lock_guard<std::mutex> lk(g_host_reg_mu);
-    auto it = g_host_reg.find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == g_host_reg.end()) return (int)MI_E_INVALID;
-    g_host_reg.erase(it);
-    g_host_reg_gen.fetch_add(1, std::memory_order_release);
-    g_host_reg_n.fetch_sub(1, std::memory_order_release);
-    return 0;
-}
+int mi_ccl_comp_unregister_host_buffer(const void* ptr) { return mi_host_undeclare(ptr); }
 
-size_t mi_ccl_comp_pointer_lookups(void) { return (size_t)t_lookups; }
+size_t mi_ccl_comp_pointer_lookups(void) { return mi_pointer_lookups(); }
 
 }  // extern "C"
 
@@ -1193,6 +1256,20 @@ size_t mi_ccl_comp_pointer_lookups(void) { return (size_t)t_lookups; }
 namespace {
 thread_local std::string t_shim_err;
 ccl_datatype mk_dtype(int dt) { return ccl_datatype(static_cast<ccl::datatype>(dt), mi_dtype_size(dt)); }
+
+// The schedule the C view passes (mi_ccl_comp_shim_sched): none, one whose
+// collective has no stream (host memory by the schedule's word), or one with
+// a stream (operands looked up).  The stream is never dereferenced.
+thread_local int t_shim_sched = 0;
+thread_local ccl_sched t_sched_host, t_sched_stream;
+ccl_sched* shim_sched() {
+    if (t_shim_sched == 1) return &t_sched_host;
+    if (t_shim_sched == 2) {
+        t_sched_stream.coll_param.stream = reinterpret_cast<ccl_stream*>(&t_sched_stream);
+        return &t_sched_stream;
+    }
+    return nullptr;
+}
 }  // namespace
 
 #define MI_SHIM_GUARD(body)                 \
@@ -1206,13 +1283,13 @@ ccl_datatype mk_dtype(int dt) { return ccl_datatype(static_cast<ccl::datatype>(d
 extern "C" {
 
 int mi_ccl_comp_reduce(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype, int op) {
-    MI_SHIM_GUARD(return (int)ccl_comp_reduce(nullptr, in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce(shim_sched(), in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
                                               static_cast<ccl::reduction>(op), nullptr, nullptr));
 }
 
 int mi_ccl_comp_reduce_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype,
                               mi_ccl_reduction_fn fn) {
-    MI_SHIM_GUARD(return (int)ccl_comp_reduce(nullptr, in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce(shim_sched(), in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
                                               ccl::reduction::custom, reinterpret_cast<ccl::reduction_fn>(fn),
                                               nullptr));
 }
@@ -1286,7 +1363,7 @@ int mi_ccl_convert_fp16_to_fp32(const void* src, void* dst) {
 
 int mi_ccl_comp_reduce_start(const void* in_buf, size_t in_count, void* inout_buf, size_t* out_count, int dtype,
                              int op, mi_ccl_reduction_fn fn, struct ccl_comp_request** req) {
-    MI_SHIM_GUARD(return (int)ccl_comp_reduce_start(in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
+    MI_SHIM_GUARD(return (int)ccl_comp_reduce_start(shim_sched(), in_buf, in_count, inout_buf, out_count, mk_dtype(dtype),
                                                     static_cast<ccl::reduction>(op),
                                                     reinterpret_cast<ccl::reduction_fn>(fn), nullptr, req));
 }
@@ -1296,7 +1373,7 @@ int mi_ccl_comp_batch_reduce_start(const void* in_buf, const size_t* offsets, si
                                    int bf16_keep_precision_mode, struct ccl_comp_request** req) {
     MI_SHIM_GUARD({
         std::vector<size_t> offs(offsets, offsets + n_offsets);
-        return (int)ccl_comp_batch_reduce_start(in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
+        return (int)ccl_comp_batch_reduce_start(shim_sched(), in_buf, offs, in_count, inout_buf, out_count, mk_dtype(dtype),
                                                 static_cast<ccl::reduction>(op), nullptr, nullptr,
                                                 bf16_keep_precision_mode, req);
     });
@@ -1325,6 +1402,13 @@ int mi_ccl_comp_request_free(struct ccl_comp_request* req) {
 }
 
 const char* mi_ccl_reduction_to_str(int op) { return ccl_reduction_to_str(static_cast<ccl::reduction>(op)); }
+
+int mi_ccl_comp_shim_sched(int mode) {
+    if (mode < 0 || mode > 2) return (int)MI_E_INVALID;
+    const int prev = t_shim_sched;
+    t_shim_sched = mode;
+    return prev;
+}
 
 int mi_ccl_env_reload(void) {
     MI_SHIM_GUARD({

@@ -20,6 +20,7 @@
 #include <sched.h>
 #include <stdexcept>
 #include <string>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/mi_reduce.h"
@@ -329,8 +330,123 @@ Kern pick(int dt, int op, unsigned v) {
 // ---------------------------------------------------------------------------
 enum PtrKind { PK_DEVICE = 0, PK_PINNED = 1, PK_PAGEABLE = 2 };
 
+// ---- declared host ranges (mi_host_declare) --------------------------------
+// HIP's pointer lookup takes a runtime-wide lock, and on pageable memory it
+// serialises concurrent callers: 0.07 us alone, 9.5 us per call at 16 threads
+// (profiles/round3_host/pointer_kind_probe_run2.jsonl).  A caller that owns
+// long-lived host buffers (oneCCL's regular_buffer_cache,
+// src/sched/buffer/buffer_cache.cpp:87-123) declares them once; classify()
+// answers for an operand lying wholly inside a declared range without asking
+// HIP.  Each range is looked up once, when declared, and keeps the kind found
+// then (device memory is refused), so a pinned range keeps its zero-copy path.
+//
+// Readers take no lock.  The ranges are an immutable sorted snapshot behind
+// an atomic pointer; a writer publishes a new one and frees the old one after
+// a grace period: every reader thread owns a slot whose counter is odd while
+// it reads, and the writer waits until each slot it saw odd has moved on.  A
+// reader that entered after the publication loads the new snapshot (both
+// sides are sequentially consistent), so nothing it can hold is freed.
+struct HostRange {
+    uintptr_t lo, hi;    // [lo, hi)
+    PtrKind kind;        // PK_PINNED or PK_PAGEABLE
+    intptr_t dev_delta;  // pinned: device-visible address - host address
+};
+struct RangeSnap {
+    std::vector<HostRange> r;  // sorted by lo, disjoint
+};
+
+std::mutex g_rng_mu;  // writers; readers without a slot
+std::atomic<const RangeSnap*> g_rng{nullptr};
+std::atomic<int> g_rng_n{0};  // ranges declared: 0 lets classify skip all of this
+
+constexpr int kReaderSlots = 256;
+struct alignas(64) ReaderSlot {
+    std::atomic<uint64_t> seq{0};  // odd: reading a snapshot
+    std::atomic<bool> used{false};
+};
+ReaderSlot g_readers[kReaderSlots];
+
+struct ReaderSlotRef {  // the calling thread's slot, released when it exits
+    int idx = -2;       // -2: not taken yet, -1: none free (read under the mutex)
+    ~ReaderSlotRef() {
+        if (idx >= 0) g_readers[idx].used.store(false, std::memory_order_release);
+    }
+};
+thread_local ReaderSlotRef t_reader;
+thread_local size_t t_lookups = 0;  // HIP pointer lookups this thread made (mi_pointer_lookups)
+
+ReaderSlot* reader_slot() {
+    if (t_reader.idx == -2) {
+        t_reader.idx = -1;
+        for (int i = 0; i < kReaderSlots; i++) {
+            bool f = false;
+            if (!g_readers[i].used.load(std::memory_order_relaxed) &&
+                g_readers[i].used.compare_exchange_strong(f, true, std::memory_order_acq_rel)) {
+                t_reader.idx = i;
+                break;
+            }
+        }
+    }
+    return t_reader.idx >= 0 ? &g_readers[t_reader.idx] : nullptr;
+}
+
+bool find_range(const RangeSnap* s, uintptr_t a, size_t bytes, HostRange* out) {
+    if (!s) return false;
+    auto it = std::upper_bound(s->r.begin(), s->r.end(), a, [](uintptr_t x, const HostRange& r) { return x < r.lo; });
+    if (it == s->r.begin()) return false;
+    --it;
+    if (a < it->lo || a >= it->hi || bytes > it->hi - a) return false;
+    *out = *it;
+    return true;
+}
+
+// [p, p + bytes) wholly inside a declared range: its kind (and, pinned, the
+// device-visible address of p)
+bool declared(const void* p, size_t bytes, PtrKind* kind, void** devptr) {
+    if (g_rng_n.load(std::memory_order_acquire) == 0) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    HostRange r;
+    bool hit;
+    if (ReaderSlot* s = reader_slot()) {
+        s->seq.fetch_add(1, std::memory_order_seq_cst);  // odd: inside
+        hit = find_range(g_rng.load(std::memory_order_seq_cst), a, bytes, &r);
+        s->seq.fetch_add(1, std::memory_order_release);
+    } else {
+        std::lock_guard<std::mutex> lk(g_rng_mu);
+        hit = find_range(g_rng.load(std::memory_order_relaxed), a, bytes, &r);
+    }
+    if (!hit) return false;
+    *kind = r.kind;
+    if (devptr && r.kind == PK_PINNED) *devptr = reinterpret_cast<void*>(a + r.dev_delta);
+    return true;
+}
+
+// Writers, under g_rng_mu: publish `next`, wait out the readers that may still
+// hold the snapshot it replaces, free that one.
+void publish_ranges(RangeSnap* next) {
+    const RangeSnap* old = g_rng.exchange(next, std::memory_order_seq_cst);
+    for (ReaderSlot& s : g_readers) {
+        if (!s.used.load(std::memory_order_seq_cst)) continue;
+        const uint64_t v = s.seq.load(std::memory_order_seq_cst);
+        if (!(v & 1)) continue;
+        while (s.seq.load(std::memory_order_acquire) == v) std::this_thread::yield();
+    }
+    delete old;
+}
+
 // `devptr` (optional): the device-visible address of a pinned host pointer.
-PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
+// `bytes`: the extent of the operand at p (for the declared ranges).
+PtrKind classify_hip(const void* p, int* dev, void** devptr);
+
+PtrKind classify(const void* p, int* dev, void** devptr = nullptr, size_t bytes = 1) {
+    PtrKind dk;
+    if (declared(p, bytes ? bytes : 1, &dk, devptr)) return dk;
+    return classify_hip(p, dev, devptr);
+}
+
+// HIP's answer (one runtime lookup, counted for mi_pointer_lookups)
+PtrKind classify_hip(const void* p, int* dev, void** devptr) {
+    t_lookups++;
     hipPointerAttribute_t at;
     memset(&at, 0, sizeof(at));
     hipError_t e = hipPointerGetAttributes(&at, p);
@@ -352,9 +468,9 @@ PtrKind classify(const void* p, int* dev, void** devptr = nullptr) {
 // A kernel may only touch device memory or pinned host memory: a pageable
 // host pointer reaching a device entry point would fault the GPU, so it is
 // refused here instead (the *_sync entry points stage pageable memory).
-int require_gpu_visible(const void* p) {
+int require_gpu_visible(const void* p, size_t bytes = 1) {
     int dev = -1;
-    if (classify(p, &dev) == PK_PAGEABLE)
+    if (classify(p, &dev, nullptr, bytes) == PK_PAGEABLE)
         return fail(MI_E_INVALID, "pageable host memory passed to a device entry point (use the *_sync form)");
     return 0;
 }
@@ -362,8 +478,11 @@ int require_gpu_visible(const void* p) {
 // ---------------------------------------------------------------------------
 // the asynchronous core: out = fold(inputs[0..k-1]) on device pointers
 // ---------------------------------------------------------------------------
+// `visible`: the caller already knows every operand is device memory or a
+// device-visible pinned address (reduce_issue classified them, or made them:
+// staging and bounce buffers), so they are not looked up again.
 int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
-                  unsigned flags, hipStream_t stream) {
+                  unsigned flags, hipStream_t stream, bool visible = false) {
     const size_t es = dtype_size(dt);
     if (!es) return fail(MI_E_INVALID, "unknown datatype");
     if (op < MI_OP_SUM || op > MI_OP_MAX) return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
@@ -373,9 +492,11 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
     for (int i = 0; i < k; i++)
         if (!inputs[i]) return fail(MI_E_INVALID, "null input");
 
-    for (int i = 0; i < k; i++)
-        if (int rc = require_gpu_visible(inputs[i])) return rc;
-    if (int rc = require_gpu_visible(out)) return rc;
+    if (!visible) {
+        for (int i = 0; i < k; i++)
+            if (int rc = require_gpu_visible(inputs[i], count * es)) return rc;
+        if (int rc = require_gpu_visible(out, count * es)) return rc;
+    }
 
     const unsigned v = canon_flags(dt, op, flags, k);
     if (k == 1 && !(v & V_ACC_FP32)) {  // nothing to combine: result is inputs[0]
@@ -514,8 +635,8 @@ int launch_reduce_batch(const mi_reduce_desc_t* d, int n, int dt, int op, unsign
     for (int i = 0; i < n; i++) {
         if (!d[i].count) continue;
         if (!d[i].in || !d[i].inout) return fail(MI_E_INVALID, "null operand in batch descriptor");
-        if (int rc = require_gpu_visible(d[i].in)) return rc;
-        if (int rc = require_gpu_visible(d[i].inout)) return rc;
+        if (int rc = require_gpu_visible(d[i].in, d[i].count * es)) return rc;
+        if (int rc = require_gpu_visible(d[i].inout, d[i].count * es)) return rc;
     }
     if (int rc = check_batch_disjoint(d, n, es)) return rc;
     const unsigned v = canon_flags(dt, op, flags, 2);
@@ -748,26 +869,53 @@ struct Drain {
 // worker runs -- holds an ExitGuard while it makes HIP calls.  An exit
 // handler, registered after the runtime's (at the first context, when HIP is
 // initialised, so it runs before the runtime's), marks the process as
-// exiting and then waits, with no time limit, until no guard is held.  A
-// section that would start after that mark makes no HIP call: a teardown
-// leaves its context to the process's end, a job fails with MI_E_EXITING.
-// The counter is raised before the mark is read (both sequentially
-// consistent), so either the section sees the mark or the handler sees the
-// section.
+// exiting and then waits until no guard is held.  A section that would start
+// after that mark makes no HIP call: a teardown leaves its context to the
+// process's end, a job fails with MI_E_EXITING.  The counter is raised before
+// the mark is read (both sequentially consistent), so either the section sees
+// the mark or the handler sees the section.
+//
+// The wait is bounded (MI_REDUCE_EXIT_WAIT_S, default 60 s): a section that
+// never ends -- a job blocked on the event of a kernel that hangs, a
+// user-supplied head fold that blocks -- would otherwise hold the process at
+// exit forever.  Past the bound the handler names the section last entered
+// and ends the process with status 70 (EX_SOFTWARE) without the runtime's
+// teardown, which would fault under the section still inside HIP.
 std::atomic<bool> g_exiting{false};
 std::atomic<int> g_active{0};
+std::atomic<const char*> g_active_what{nullptr};  // the section most recently entered
+
+double exit_wait_s() {
+    const char* e = getenv("MI_REDUCE_EXIT_WAIT_S");
+    const double v = e ? atof(e) : 60.0;
+    return v > 0 ? v : 60.0;
+}
 
 void at_process_exit() {
     g_exiting.store(true);
-    while (g_active.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    const double limit = exit_wait_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (g_active.load() > 0) {
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+            const char* what = g_active_what.load();
+            fprintf(stderr,
+                    "oneccl_amd: process exit: %d library section(s) still running after %.0f s (last entered: %s); "
+                    "ending the process without the HIP runtime's teardown\n",
+                    g_active.load(), limit, what ? what : "?");
+            fflush(nullptr);
+            _exit(70);
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
 }
 
 struct ExitGuard {
     bool entered;
-    ExitGuard() {
+    explicit ExitGuard(const char* what) {
         g_active.fetch_add(1);
         entered = !g_exiting.load();
         if (!entered) g_active.fetch_sub(1);
+        else g_active_what.store(what);
     }
     ~ExitGuard() {
         if (entered) g_active.fetch_sub(1);
@@ -779,7 +927,7 @@ struct ExitGuard {
 struct ThreadCtx {
     std::vector<DevCtx*> devs;
     ~ThreadCtx() {
-        ExitGuard g;
+        ExitGuard g("a thread's HIP context teardown");
         if (g.entered)
             for (DevCtx* d : devs) delete d;
     }
@@ -892,7 +1040,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     for (int i = 0; i < k; i++) {
         void* dp = const_cast<void*>(inputs[i]);
         int d_i = -1;
-        kin[i] = classify(inputs[i], &d_i, &dp);
+        kin[i] = classify(inputs[i], &d_i, &dp, count * es);
         dins[i] = dp;
         all_dev = all_dev && kin[i] == PK_DEVICE;
         if (d_i >= 0) {
@@ -902,7 +1050,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     }
     void* dout = out;
     int d_o = -1;
-    const PtrKind kout = classify(out, &d_o, &dout);
+    const PtrKind kout = classify(out, &d_o, &dout, count * es);
     all_dev = all_dev && kout == PK_DEVICE;
     if (d_o >= 0) {
         mixed_dev = mixed_dev || (pdev >= 0 && d_o != pdev);
@@ -939,7 +1087,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
             MI_HIP(hipEventCreateWithFlags(t_start, hipEventDefault));
             MI_HIP(hipEventRecord(*t_start, d->stream[0]));
         }
-        return launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0]);
+        return launch_reduce(dins, k, dout, count, dt, op, flags, d->stream[0], true);
     }
 
     // small pageable operands (synchronous callers only): CPU copy into
@@ -964,7 +1112,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         for (int i = 0; i < k; i++) bins[i] = kin[i] == PK_PAGEABLE ? bounce_of(inputs[i], true) : dins[i];
         void* bout = kout == PK_PAGEABLE ? bounce_of(out, false) : dout;
         *used = 1;
-        rc = launch_reduce(bins, k, bout, count, dt, op, flags, d->stream[0]);
+        rc = launch_reduce(bins, k, bout, count, dt, op, flags, d->stream[0], true);
         if (rc) return rc;
         if (kout == PK_PAGEABLE) *post = HostCopy{out, bout, count * es};
         return 0;
@@ -1029,7 +1177,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         // last chunk holds elements >= (count/16)*16, and chunk starts are
         // multiples of 16, so the per-chunk split computed inside
         // launch_reduce is the same split.
-        rc = launch_reduce(din, k, cdst, n, dt, op, flags, st);
+        rc = launch_reduce(din, k, cdst, n, dt, op, flags, st, true);
         if (rc) return rc;
         if (slot_of[k] >= 0) {
             if (drained) {
@@ -1160,7 +1308,7 @@ struct StageWorker {
             }
             int rc = 0;
             {
-                ExitGuard g;  // the exit handler waits for a job that has started
+                ExitGuard g("a staging worker's job");  // the exit handler waits for a job that has started
                 if (!g.entered) {
                     rc = fail(MI_E_EXITING, "the process is exiting: asynchronous request not run");
                     j->prior.clear();  // their events go with the process
@@ -1285,11 +1433,11 @@ std::vector<hipEvent_t> record_prior() {
 
 // Does a fold over these operands need host staging (pageable operands, or
 // pinned ones under MI_HOST_STAGED)?
-bool needs_staging(const void* const* inputs, int k, const void* out) {
+bool needs_staging(const void* const* inputs, int k, const void* out, size_t bytes) {
     const bool staged_mode = host_mode() == MI_HOST_STAGED;
     for (int i = 0; i <= k; i++) {
         int dev = -1;
-        const PtrKind kind = classify(i < k ? inputs[i] : out, &dev);
+        const PtrKind kind = classify(i < k ? inputs[i] : out, &dev, nullptr, bytes);
         if (kind == PK_PAGEABLE || (kind == PK_PINNED && staged_mode)) return true;
     }
     return false;
@@ -1432,7 +1580,8 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
         if (count == 0) return 0;
         if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
         int pdev = -1;
-        const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+        const PtrKind ks = classify(src, &pdev, nullptr, count * dtype_size(src_dtype)),
+                      kd = classify(dst, &pdev, nullptr, count * dtype_size(dst_dtype));
         if (device < 0 && pdev >= 0) device = pdev;
         DevCtx* d = nullptr;
         int rc = get_ctx(device, &d);
@@ -1512,7 +1661,7 @@ int reduce_start(const void* const* inputs, int k, void* out, size_t count, int 
             // worker still has requests of this thread, later requests go
             // there too, so a thread's requests run in submission order
             // whatever their pointer kinds.
-            if (needs_staging(inputs, k, out) || t_stage.busy()) {
+            if (needs_staging(inputs, k, out, count * dtype_size(dtype)) || t_stage.busy()) {
                 auto j = std::make_shared<AsyncJob>();
                 j->prior = record_prior();
                 for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
@@ -1819,7 +1968,7 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
         if (bytes == 0) return 0;
         if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
         int pdev = -1;
-        const PtrKind ks = classify(src, &pdev), kd = classify(dst, &pdev);
+        const PtrKind ks = classify(src, &pdev, nullptr, bytes), kd = classify(dst, &pdev, nullptr, bytes);
         if (device < 0 && pdev >= 0) device = pdev;
         DevCtx* d = nullptr;
         int rc = get_ctx(device, &d);
@@ -1896,6 +2045,87 @@ int mi_pointer_kind(const void* ptr, int* device) {
     const int kind = (int)classify(ptr, &dev);
     if (device) *device = dev;
     return kind;
+}
+
+int mi_pointer_kind_range(const void* ptr, size_t bytes, int* device) {
+    int dev = -1;
+    const int kind = (int)classify(ptr, &dev, nullptr, bytes);
+    if (device) *device = dev;
+    return kind;
+}
+
+int mi_host_declare(const void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return fail(MI_E_INVALID, "null / empty range");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    if (bytes > UINTPTR_MAX - a) return fail(MI_E_INVALID, "range wraps the address space");
+    // one lookup of each end, outside the writers' lock: both ends must be
+    // host memory of one kind, and a pinned range one mapping
+    const uintptr_t last = a + bytes - 1;
+    int d0 = -1, d1 = -1;
+    void* v0 = const_cast<void*>(ptr);
+    void* v1 = reinterpret_cast<void*>(last);
+    const PtrKind k0 = classify_hip(ptr, &d0, &v0), k1 = classify_hip(v1, &d1, &v1);
+    if (k0 == PK_DEVICE || k1 == PK_DEVICE)
+        return fail(MI_E_INVALID, "device or managed memory cannot be declared as host memory");
+    if (k0 != k1) return fail(MI_E_INVALID, "the range spans pinned and pageable memory");
+    const intptr_t delta = (intptr_t)(reinterpret_cast<uintptr_t>(v0) - a);
+    if (k0 == PK_PINNED && (intptr_t)(reinterpret_cast<uintptr_t>(v1) - last) != delta)
+        return fail(MI_E_INVALID, "the pinned range spans several mappings");
+    try {
+        std::lock_guard<std::mutex> lk(g_rng_mu);
+        const RangeSnap* cur = g_rng.load(std::memory_order_relaxed);
+        std::unique_ptr<RangeSnap> next(new RangeSnap);
+        if (cur) next->r = cur->r;
+        auto it = std::upper_bound(next->r.begin(), next->r.end(), a,
+                                   [](uintptr_t x, const HostRange& r) { return x < r.lo; });
+        if (it != next->r.end() && it->lo < a + bytes) return fail(MI_E_INVALID, "overlaps a declared range");
+        if (it != next->r.begin() && std::prev(it)->hi > a) return fail(MI_E_INVALID, "overlaps a declared range");
+        next->r.insert(it, HostRange{a, a + bytes, k0, k0 == PK_PINNED ? delta : 0});
+        publish_ranges(next.release());
+        g_rng_n.fetch_add(1, std::memory_order_release);
+    } catch (const std::exception&) {
+        return fail(MI_E_RESOURCE, "out of memory");
+    }
+    return 0;
+}
+
+int mi_host_undeclare(const void* ptr) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    try {
+        std::lock_guard<std::mutex> lk(g_rng_mu);
+        const RangeSnap* cur = g_rng.load(std::memory_order_relaxed);
+        if (!cur) return fail(MI_E_INVALID, "not a declared range");
+        auto it = std::lower_bound(cur->r.begin(), cur->r.end(), a,
+                                   [](const HostRange& r, uintptr_t x) { return r.lo < x; });
+        if (it == cur->r.end() || it->lo != a) return fail(MI_E_INVALID, "not a declared range");
+        std::unique_ptr<RangeSnap> next(new RangeSnap);
+        next->r.reserve(cur->r.size() - 1);
+        for (const HostRange& r : cur->r)
+            if (r.lo != a) next->r.push_back(r);
+        g_rng_n.fetch_sub(1, std::memory_order_release);
+        publish_ranges(next.release());
+    } catch (const std::exception&) {
+        return fail(MI_E_RESOURCE, "out of memory");
+    }
+    return 0;
+}
+
+int mi_host_declared_kind(const void* ptr, size_t bytes) {
+    PtrKind k;
+    return declared(ptr, bytes ? bytes : 1, &k, nullptr) ? (int)k : -1;
+}
+
+size_t mi_pointer_lookups(void) { return t_lookups; }
+
+int mi_test_hold_exit_guard(int hold_ms) {
+    ensure_exit_hook();
+    std::thread([hold_ms] {
+        ExitGuard g("mi_test_hold_exit_guard");
+        if (hold_ms < 0)
+            for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+        std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
+    }).detach();
+    return 0;
 }
 
 size_t mi_dtype_size(int dtype) { return dtype_size(dtype); }

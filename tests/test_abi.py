@@ -67,7 +67,7 @@ def test_shim_exports_async_entry_points():
     """The asynchronous form declared in include/mi_ccl_comp_async.hpp."""
     out = subprocess.run(["nm", "-DC", "--defined-only", str(ROOT / "oneccl_amd/lib/libccl_comp_hip.so")],
                          check=True, capture_output=True, text=True).stdout
-    for w in ["ccl_comp_reduce_start(void const*, unsigned long, void*, unsigned long*, ccl_datatype const&, "
+    for w in ["ccl_comp_reduce_start(ccl_sched*, void const*, unsigned long, void*, unsigned long*, ccl_datatype const&, "
               "ccl::v1::reduction, void (*)(void const*, unsigned long, void*, unsigned long*, ccl::v1::datatype, "
               "ccl::v1::fn_context const*), ccl::v1::fn_context const*, ccl_comp_request**)",
               "ccl_comp_request_test(ccl_comp_request*)", "ccl_comp_request_wait(ccl_comp_request*)",

@@ -1,0 +1,141 @@
+"""Declared host ranges on the GPU:
+a registration is validated once -- device memory refused, pinned memory kept
+pinned so the zero-copy kernel reads it in place -- and every classification
+after it, the dispatcher's and the GPU path's (reduce_issue), answers from
+the range without HIP's pointer lookup.  Bits against the oracle."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oneccl_amd import _lib, comp
+from tests.util import BF16, FP32, assert_same, rand_array
+
+pytestmark = pytest.mark.gpu
+
+MI_E_INVALID = -1
+
+
+@pytest.fixture()
+def gpu_dispatch():
+    """The GPU paths for host buckets of any size (CCL_COMP_HOST_MAX_BYTES=0)."""
+    saved = os.environ.get("CCL_COMP_HOST_MAX_BYTES")
+    os.environ["CCL_COMP_HOST_MAX_BYTES"] = "0"
+    comp.env_reload()
+    yield
+    if saved is None:
+        os.environ.pop("CCL_COMP_HOST_MAX_BYTES", None)
+    else:
+        os.environ["CCL_COMP_HOST_MAX_BYTES"] = saved
+    comp.env_reload()
+
+
+def _impls():
+    b, f = comp.impl_types()
+    return int(b), int(f)
+
+
+def test_device_memory_is_refused():
+    import torch
+    shim = _lib.shim()
+    t = torch.zeros(1 << 16, dtype=torch.float32, device="cuda")
+    assert shim.mi_ccl_comp_register_host_buffer(t.data_ptr(), t.numel() * 4) == MI_E_INVALID
+    assert b"device" in _lib.mi().mi_last_error()
+    assert _lib.mi().mi_host_declared_kind(t.data_ptr(), 64) == -1
+    # a host range that runs into device memory is refused too (its last byte)
+    assert shim.mi_ccl_comp_register_host_buffer(t.data_ptr() + 4096, 16) == MI_E_INVALID
+
+
+@pytest.mark.parametrize("dt,n", [(FP32, 4099), (FP32, (40 << 20) // 4 + 33), (BF16, 300001)])
+def test_pinned_registration_keeps_zero_copy(gpu_dispatch, dt, n):
+    import torch
+    shim, m = _lib.shim(), _lib.mi()
+    b_impl, f_impl = _impls()
+    a = rand_array(dt, n, seed=71, specials=False)
+    b = rand_array(dt, n, seed=72, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, b_impl, f_impl)
+    ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+    hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+    pa, pb = ha.data_ptr(), hb.data_ptr()
+    assert shim.mi_ccl_comp_register_host_buffer(pa, a.nbytes) == 0
+    assert shim.mi_ccl_comp_register_host_buffer(pb, b.nbytes) == 0
+    try:
+        assert m.mi_host_declared_kind(pa, a.nbytes) == 1 and m.mi_host_declared_kind(pb, b.nbytes) == 1
+        dev = ctypes.c_int(-1)
+        assert m.mi_pointer_kind_range(pa + 64, 64, ctypes.byref(dev)) == 1
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        comp.comp_reduce(pa, n, pb, comp.datatype(dt), comp.reduction.sum)
+        assert shim.mi_ccl_comp_pointer_lookups() == n0  # the shim's and the GPU path's classification
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(pa) == 0
+        assert shim.mi_ccl_comp_unregister_host_buffer(pb) == 0
+    got = hb.numpy().view(a.dtype)
+    assert_same(got, exp, dt)
+
+
+@pytest.mark.parametrize("n", [4099, (40 << 20) // 4 + 33])
+def test_registered_pageable_gpu_paths_make_no_lookup(gpu_dispatch, n):
+    """Pageable operands inside registered buffers: bounce buffers (small),
+    the staged pipeline (past one chunk); the lookup count covers
+    libmi_reduce's classify() as well as the shim's."""
+    shim = _lib.shim()
+    b_impl, f_impl = _impls()
+    a = rand_array(FP32, n, seed=81, specials=False)
+    b = rand_array(FP32, n, seed=82, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8, b_impl, f_impl)
+    assert shim.mi_ccl_comp_register_host_buffer(a.ctypes.data, a.nbytes) == 0
+    assert shim.mi_ccl_comp_register_host_buffer(b.ctypes.data, b.nbytes) == 0
+    try:
+        n0 = shim.mi_ccl_comp_pointer_lookups()
+        comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype(FP32), comp.reduction.sum)
+        assert shim.mi_ccl_comp_pointer_lookups() == n0
+    finally:
+        assert shim.mi_ccl_comp_unregister_host_buffer(a.ctypes.data) == 0
+        assert shim.mi_ccl_comp_unregister_host_buffer(b.ctypes.data) == 0
+    assert_same(b, exp, FP32)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_host_schedule_large_bucket_bits(mode):
+    """Above the dispatcher's threshold a host schedule's bucket is split
+    between the calling thread and the GPU as before (its kinds are looked up
+    then: pinned vs pageable picks the GPU route); bits are the oracle's in
+    every schedule mode."""
+    shim = _lib.shim()
+    b_impl, f_impl = _impls()
+    n = (48 << 20) // 4 + 5
+    a = rand_array(FP32, n, seed=90 + mode, specials=False)
+    b = rand_array(FP32, n, seed=95 + mode, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a, exp, FP32, 0, 8, b_impl, f_impl)
+    prev = shim.mi_ccl_comp_shim_sched(mode)
+    try:
+        comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype(FP32), comp.reduction.sum)
+    finally:
+        shim.mi_ccl_comp_shim_sched(prev)
+    assert_same(b, exp, FP32)
+
+
+def test_device_operands_under_a_stream_schedule():
+    """A schedule with a stream may hand device memory (the reference's SYCL
+    branch, comp.cpp:144-195): the operands are looked up and reduced on the
+    GPU in place."""
+    import torch
+    shim = _lib.shim()
+    n = 1 << 20
+    a = torch.rand(n, device="cuda")
+    b = torch.rand(n, device="cuda")
+    exp = (b + a).cpu()
+    prev = shim.mi_ccl_comp_shim_sched(2)
+    try:
+        comp.comp_reduce(a.data_ptr(), n, b.data_ptr(), comp.datatype(FP32), comp.reduction.sum)
+    finally:
+        shim.mi_ccl_comp_shim_sched(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(b.cpu().view(torch.int32), exp.view(torch.int32))

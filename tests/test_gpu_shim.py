@@ -860,8 +860,9 @@ print("exit-async: ok", flush=True)
 def test_process_exit_with_unwaited_async_requests():
     """process exit while a thread's staging worker still runs
     its un-waited asynchronous requests (profiles/round2_dispatch/
-    exit_crash_trace.txt).  The exit handler now waits, without a time cap,
-    for every job in progress; jobs not yet started are dropped."""
+    exit_crash_trace.txt).  The exit handler waits for every job in progress
+    (bounded by MI_REDUCE_EXIT_WAIT_S, tests/test_exit_guard.py); jobs not yet
+    started are dropped."""
     import subprocess
     import sys
     from pathlib import Path
@@ -879,7 +880,8 @@ def test_registered_pageable_on_gpu_paths(n, dt):
     """Pageable operands inside registered host buffers
     (mi_ccl_comp_register_host_buffer) take the GPU paths — bounce buffers for
     small buckets, the staged pipeline past one chunk — with the oracle's bits
-    and without HIP's pointer lookup."""
+    and without HIP's pointer lookup, in the shim or in libmi_reduce's GPU path
+    (one counter, mi_pointer_lookups)."""
     shim = _lib.shim()
     b_impl, f_impl = impls()
     a = rand_array(dt, n, seed=91, specials=False)

@@ -15,6 +15,7 @@ reference tree is only read.  Runs where /root/reference exists.
   0002  atl_mpi_ctx.cpp           MPI fp16 user op through ccl_fp16_reduce          (§2b)
   0003  reduce_local_entry, recv_reduce_entry: start the reduce, poll it        (§2d)
   0004  allreduce.cpp nreduce + entry_factory.hpp: one fused fan-in per segment (§2e)
+  0005  buffer_cache.cpp: the regular buffer cache declares its host buffers     (§2f)
 """
 from __future__ import annotations
 
@@ -40,6 +41,7 @@ UNITS = {  # translation units the patches touch (headers through their includer
     "reduce_local_entry": "src/sched/entry/reduce_local_entry.cpp",
     "allreduce": "src/coll/algorithms/allreduce/allreduce.cpp",  # recv_reduce_entry.hpp, entry_factory.hpp
     "atl_mpi_ctx": "src/atl/mpi/atl_mpi_ctx.cpp",
+    "buffer_cache": "src/sched/buffer/buffer_cache.cpp",
 }
 
 
@@ -85,7 +87,8 @@ def objs(tree, tmp_path_factory):
 def test_patch_set_is_complete():
     names = [p.name for p in PATCHES]
     assert names == ["0001-build-swap-src-comp.patch", "0002-atl-mpi-fp16-user-op.patch",
-                     "0003-async-host-reduce-entries.patch", "0004-nreduce-fused-fanin.patch"], names
+                     "0003-async-host-reduce-entries.patch", "0004-nreduce-fused-fanin.patch",
+                     "0005-buffer-cache-declares-host-buffers.patch"], names
     assert (NEW_FILES / "sched" / "entry" / "batch_reduce_entry.hpp").exists()
 
 
@@ -127,6 +130,26 @@ def test_patched_units_need_only_what_the_dropin_defines(objs):
     starts = {s for s in _undefs(objs["reduce_local_entry"][0]) if "ccl_comp_reduce_start" in s}
     assert starts, "reduce_local_entry must start the reduce asynchronously"
     assert any("ccl_comp_batch_reduce_start" in s for s in _undefs(objs["allreduce"][0]))
+    # the schedule reaches the asynchronous entries (its stream decides
+    # whether operands are looked up): ccl_sched* is their first parameter
+    assert all("P9ccl_sched" in s for s in starts), starts
     fp16 = {s for s in _undefs(objs["atl_mpi_ctx"][0]) if "fp16" in s}
     assert any("ccl_fp16_reduce" in s for s in fp16)
     assert not any("wrap" in s for s in fp16), fp16  # the inline SIMD body is no longer used
+
+
+def test_buffer_cache_declares_exactly_what_it_frees(tree, objs):
+    """0005: every buffer the regular cache mallocs is declared, and every
+    CCL_FREE of one (clear() and push() without the cache) undeclares it
+    first; the declaration symbols it needs are the drop-in's C exports."""
+    d, _ = tree
+    src = (d / "src" / "sched" / "buffer" / "buffer_cache.cpp").read_text()
+    body = src[src.index("void regular_buffer_cache::clear()"):src.index("#ifdef CCL_ENABLE_SYCL\nsycl_buffer_cache")]
+    assert body.count("CCL_MALLOC") == 1 and body.count("mi_ccl_comp_register_host_buffer(*pptr, bytes)") == 1
+    assert body.count("CCL_FREE") == 2
+    for free_at in [m.start() for m in re.finditer(r"CCL_FREE\(", body)]:
+        before = body[:free_at].rstrip().splitlines()[-1]
+        assert "mi_ccl_comp_unregister_host_buffer" in before, before
+    need = _undefs(objs["buffer_cache"][0])
+    assert {"mi_ccl_comp_register_host_buffer", "mi_ccl_comp_unregister_host_buffer"} <= need
+    assert {"mi_ccl_comp_register_host_buffer", "mi_ccl_comp_unregister_host_buffer"} <= _global_defs(objs["ours"][0])

@@ -91,6 +91,18 @@ for step in "$@"; do
                 run "small_workers_$T" 120 ./tools/small_workers $T 1024 &&
                 run "small_workers_reg_$T" 120 ./tools/small_workers $T 1024 reg
             done ;;
+        smallw)  # 4 KiB / 64 KiB / 512 KiB host chunks at T workers: drop-in (lookups, registry, host
+                 # schedule) against the reference's own compiled CPU loop, one JSON line each
+            for n in ${SMALLW_ELEMS:-1024 16384 131072}; do
+                for T in 1 2 4 8 16; do
+                    for mode in ${SMALLW_MODES:-default reg sched ref}; do
+                        timeout -k 10 120 ./tools/small_workers $T $n $mode >> "$OUT/smallw.jsonl" 2>> "$OUT/smallw.err"
+                        rc=$?
+                        [ $rc -eq 0 ] || { echo "STOP: smallw $T $n $mode rc=$rc" | tee -a "$OUT/steps.log"; exit $rc; }
+                    done
+                done
+                echo "=== smallw n=$n done" | tee -a "$OUT/steps.log"
+            done ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)
