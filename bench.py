@@ -308,7 +308,69 @@ def timed_steps(step, steps, warmup, stream, world, probe=10):
     return elapsed, avg_ms, [a.elapsed_time(b) for a, b in ev]
 
 
-def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None):
+CEILING_LIB = "oneccl_amd/lib/libmi_ceiling.so"
+
+
+def measured_ceiling(ins, k, nbytes, stream, launches=10):
+    """The achievable ceiling of a k-input reduce on these buffers, in this
+    process: the fastest a memory-only kernel reads the k
+    input streams (tools/ceiling_probe.hip mic_read_streams: 16-byte
+    non-temporal loads, nothing written) and writes one stream
+    (mic_write_stream), each over a few launch shapes, best shape taken.
+    Reads and writes share HBM, so the reduce's k reads + 1 write cannot
+    beat (k + 1) * nbytes / (t_read + t_write).  Writes over ins[0] (the
+    caller refills before its parity check).  None if the probe library is
+    missing (it is measurement infrastructure, not product)."""
+    import ctypes
+
+    import torch
+    path = ROOT / CEILING_LIB
+    if not path.exists():
+        return None
+    L = ctypes.CDLL(str(path))
+    L.mic_read_streams.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.mic_write_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    from oneccl_amd import _lib
+    waves = ctypes.c_int(0)
+    _lib.check(_lib.mi().mi_get_residency(-1, k, ctypes.byref(waves), None), "mi_get_residency")
+    shapes = [(64, waves.value), (64, 0), (256, 0), (1024, 0)]
+    arr = _lib.void_ptr_array([t.data_ptr() for t in ins[:k]])
+    sink = torch.zeros(1024, dtype=torch.int32, device=ins[0].device)
+    sh = stream.cuda_stream
+    nb = nbytes - nbytes % 16
+
+    def best(launch):
+        res = []
+        for block, w in shapes:
+            for _ in range(2):
+                if launch(block, w):
+                    break
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(launches):
+                    launch(block, w)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                res.append((e0.elapsed_time(e1) / launches, block, w))
+        return min(res) if res else None
+
+    r = best(lambda b, w: L.mic_read_streams(arr, k, nb, b, w, sink.data_ptr(), sh))
+    wr = best(lambda b, w: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, sh))
+    if not r or not wr:
+        return None
+    t = (r[0] + wr[0]) / 1e3
+    return {"ceiling_TBps": round((k + 1) * nb / t / 1e12, 3),
+            "read_TBps": round(k * nb / (r[0] / 1e3) / 1e12, 3), "read_shape": [r[1], r[2]],
+            "write_TBps": round(nb / (wr[0] / 1e3) / 1e12, 3), "write_shape": [wr[1], wr[2]],
+            "method": f"memory-only probes on this leg's buffers (tools/ceiling_probe.hip): {k} read streams and one "
+                      "write stream, each timed alone over block x wave-cap shapes [block, waves/CU (0 = no cap)], "
+                      "best shape; ceiling = (k+1) x bytes / (t_read + t_write)"}
+
+
+def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None,
+                 n_devices=None):
     """One bucket of n_total elements split by element range over the ranks
     (mi_shard_range, 256-element aligned; BASELINE configs[3] as written):
     this rank reduces its shard of all k inputs.  `ins` (optional) holds
@@ -338,9 +400,9 @@ def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, w
             "ms_per_step": round(elapsed / steps * 1e3, 4),
             "avg_kernel_ms_max_rank": round(avg_ms_max, 5),
             "aggregate_roofline": {"achieved": round((k + 1) * total_bytes / (avg_ms_max / 1e3) / 1e9, 1),
-                                   "peak": HBM_PEAK_GBPS * world,
+                                   "peak": HBM_PEAK_GBPS * (n_devices or world),
                                    "frac": round((k + 1) * total_bytes / (avg_ms_max / 1e3) / 1e9 /
-                                                 (HBM_PEAK_GBPS * world), 4)},
+                                                 (HBM_PEAK_GBPS * (n_devices or world)), 4)},
             "per_rank_launch_bytes": algo,
             "scaling": "strong", "note": "one bucket split by element range over the ranks, no collective"}
 
@@ -382,11 +444,16 @@ def config_legs(m, stream, launches=10):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / launches
         algo = (k + 1) * n * es
+        ceil = measured_ceiling(ins, k, n * es, stream)
         par = full_parity(lambda: _lib.check(step(), name), ins, k, dt, op, flags, 0xE0, "mi_reduce" if k == 2 else
                           "mi_reduce_multi")
         legs[name] = {"workload": desc, "GiBps": round(bucket / GiB / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
                       "roofline_frac": round(algo / (ms / 1e3) / (HBM_PEAK_GBPS * 1e9), 4),
                       "parity": {"elements": par["elements"], "mismatches": par["mismatches"]}}
+        if ceil:
+            legs[name]["ceiling_TBps"] = ceil["ceiling_TBps"]
+            legs[name]["frac_of_ceiling"] = round(algo / (ms / 1e3) / 1e12 / ceil["ceiling_TBps"], 4)
+            legs[name]["ceiling"] = ceil
         del ins, arr
         torch.cuda.empty_cache()
     # C1: host buffers through the drop-in entry point
@@ -501,6 +568,24 @@ def launch_ranks(plans, timeout=None):
     return failed if failed >= 0 else 128 - failed  # killed by signal s -> 128 + s
 
 
+def device_identity(index):
+    """A physical device's identity: PCI domain:bus:device and UUID when the
+    runtime reports them (ranks on one GPU share it)."""
+    import torch
+    p = torch.cuda.get_device_properties(index)
+    pci = ":".join(f"{getattr(p, a, -1):x}" for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    return f"{pci}/{getattr(p, 'uuid', '')}"
+
+
+def device_plan(idents):
+    """From every rank's device identity: (distinct devices, max ranks on one
+    device, rehearsal?).  A shared device makes the N-rank line a rehearsal:
+    n_gpus counts devices, not ranks, and the aggregate peak is theirs."""
+    from collections import Counter
+    c = Counter(idents)
+    return len(c), max(c.values()), len(c) < len(idents)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -510,7 +595,11 @@ def main():
         argv = sys.argv[1:]
         ndev = torch.cuda.device_count()
         if args.dist_backend == "nccl" and ndev < args.gpus:
-            log(f"note: {args.gpus} ranks but {ndev} visible GPU(s): ranks share GPUs over a gloo process group")
+            # RCCL takes one rank per GPU: with fewer GPUs than ranks this can
+            # only be a rehearsal of the N-rank path, ranks sharing GPUs over a
+            # gloo group; the line says so ("rehearsal": true, n_gpus = the
+            # distinct devices, peak = those devices' HBM)
+            log(f"note: {args.gpus} ranks but {ndev} visible GPU(s): a REHEARSAL, ranks share GPUs over gloo")
             argv += ["--dist-backend", "gloo"]
         sys.exit(launch_ranks(rank_plan(args.gpus, argv, free_port())))
     import torch
@@ -532,6 +621,12 @@ def main():
             dist.init_process_group("gloo")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     pg_world = dist.get_world_size() if world > 1 else 1  # the ranks the process group saw
+    ident = device_identity(torch.cuda.current_device())
+    idents = [ident]
+    if world > 1:
+        idents = [None] * pg_world
+        dist.all_gather_object(idents, ident)
+    n_devices, ranks_per_device, rehearsal = device_plan(idents)
 
     cfg = CONFIGS[args.config]
     desc, dt, es, op, k, bucket, flags = cfg
@@ -558,6 +653,9 @@ def main():
 
     elapsed, avg_kern_ms, kern_ms = timed_steps(step, args.steps, args.warmup, stream, world)
     elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, coll_dev)
+    # the achievable ceiling on these buffers (outside the timed region;
+    # overwrites ins[0], which full_parity refills)
+    ceil = measured_ceiling(ins, k, n * es, stream)
 
     # the whole bucket checked bit for bit, outside the timed region (every
     # rank checks its own; the line reports the sum over ranks)
@@ -572,6 +670,7 @@ def main():
     # whole job: all ranks' launch bytes over the slowest rank's launch time,
     # against world x one HBM (north star: fraction of aggregate HBM roofline)
     agg_achieved = (k + 1) * total_bytes / (avg_kern_ms_max / 1e3) / 1e9
+    agg_peak = HBM_PEAK_GBPS * n_devices  # the distinct devices' HBM, not ranks x one HBM
 
     # the same bucket through oneCCL's own entry point: ccl_comp_reduce of the
     # drop-in shim (synchronous, as src/sched calls it) — reported beside `value`
@@ -610,8 +709,13 @@ def main():
         host_leg = host_resident_leg(m, dt, es, op, flags, min(n, (256 << 20) // es))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if world > 1:
+        dist.barrier()  # every rank is past its timed region before rank 0 loads the host cores
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, args.cpu_seconds)
+        if world > 1:
+            cpu["note_n_gpus"] = (f"measured on rank 0 after the {world}-rank timed region and a barrier, while the "
+                                  "other ranks idle; the same bounded sample as at N=1")
 
     legs = None
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_config_legs:
@@ -623,11 +727,11 @@ def main():
     strong = None
     if world > 1 and args.config == "c2":
         strong = {"c2": strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, args.steps,
-                                     args.warmup, coll_dev, ins=ins)}
+                                     args.warmup, coll_dev, ins=ins, n_devices=n_devices)}
         del ins
         torch.cuda.empty_cache()
         strong["c4_fanin8"] = strong_split(m, 9, 4, 0, 8, 0, GiB // 4, rank, world, stream, args.steps,
-                                           args.warmup, coll_dev)
+                                           args.warmup, coll_dev, n_devices=n_devices)
         torch.cuda.empty_cache()
 
     traffic = pmc_traffic(args.config, traffic_per_launch)
@@ -637,7 +741,9 @@ def main():
             if args.config == "c2" else f"GiB/s device-resident {args.config} bucket reduce",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": pg_world,
+            "n_gpus": n_devices,
+            "ranks": pg_world,
+            "ranks_per_device": ranks_per_device,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -658,9 +764,10 @@ def main():
                          "avg_kernel_ms": round(avg_kern_ms, 5), "avg_kernel_ms_max_rank": round(avg_kern_ms_max, 5),
                          "kernel_ms_min": round(min(kern_ms), 5),
                          "kernel_ms_probe": [round(x, 5) for x in kern_ms],
-                         "aggregate": {"achieved": round(agg_achieved, 1), "peak": HBM_PEAK_GBPS * world,
-                                       "frac": round(agg_achieved / (HBM_PEAK_GBPS * world), 4),
-                                       "note": "all ranks' algorithmic launch bytes / max-over-ranks mean launch time"},
+                         "aggregate": {"achieved": round(agg_achieved, 1), "peak": agg_peak,
+                                       "frac": round(agg_achieved / agg_peak, 4), "devices": n_devices,
+                                       "note": "all ranks' algorithmic launch bytes / max-over-ranks mean launch "
+                                               "time, against the distinct devices' HBM"},
                          "timing": "one hipEvent pair on the launch stream around the K back-to-back timed launches "
                                    "(avg_kernel_ms = that time / K, inter-launch gaps included); kernel_ms_min/_probe: "
                                    "10 launches each between their own event pair, after the timed region",
@@ -668,6 +775,14 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if ceil:
+            out["roofline"]["ceiling_TBps"] = ceil["ceiling_TBps"]
+            out["roofline"]["frac_of_ceiling"] = round(achieved / 1e3 / ceil["ceiling_TBps"], 4)
+            out["roofline"]["ceiling"] = ceil
+        if rehearsal:
+            out["rehearsal"] = True
+            out["rehearsal_note"] = (f"{pg_world} ranks on {n_devices} device(s): a rehearsal of the N-rank path, "
+                                     "not an N-GPU measurement (ranks share a GPU's HBM)")
         if strong:
             out["strong_split"] = strong
         if dropin:

@@ -160,6 +160,27 @@ def build_pointer_kind_probe(force: bool = False) -> Path:
     return out
 
 
+def build_ceiling(force: bool = False) -> Path:
+    """libmi_ceiling.so: the memory-only probes bench.py prices each kernel's
+    measured ceiling with (tools/ceiling_probe.hip; not product code)."""
+    out = LIB / "libmi_ceiling.so"
+    src = ROOT / "tools" / "ceiling_probe.hip"
+    if src.exists() and (force or _stale(out, [src])):
+        LIB.mkdir(exist_ok=True)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+              "-o", str(out), str(src)])
+    return out
+
+
+def build_residency_probe(force: bool = False) -> Path:
+    """Probe: resident one-wave workgroups per CU against a dynamic LDS size."""
+    out = ROOT / "tools" / "residency_probe"
+    src = ROOT / "tools" / "residency_probe.hip"
+    if src.exists() and (force or _stale(out, [src])):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-o", str(out), str(src)])
+    return out
+
+
 def build_small_workers(force: bool = False) -> Path:
     """Probe: small host reduces through the drop-in from T threads at once."""
     out = ROOT / "tools" / "small_workers"
@@ -250,6 +271,7 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_shim(force)
     build_dropin_caller(force)
     build_oracle(force)
+    build_ceiling(force)
     build_sweep()
     build_policy_sweep()
     build_fan_sweep()
@@ -260,6 +282,7 @@ def build_all(force: bool = False, asan: bool = False) -> None:
     build_latency()
     build_pointer_kind_probe()
     build_small_workers()
+    build_residency_probe()
     build_segv_trace()
     if asan:
         build_asan(force)

@@ -20,8 +20,14 @@
 // reduce and returns `started`; the worker's progress loop calls update()
 // until the entry is complete (src/sched/entry/reduce_local_entry.cpp:116-131,
 // src/exec/thread/worker.cpp:310-379).
+// The entry's schedule goes along, as the patched entries pass it: a
+// collective without a stream works on host memory (nothing is looked up),
+// one with a stream may hand device memory (src/comp/comp.cpp:136-142).
 enum entry_status { not_started, started, complete };
+static ccl_sched g_host_sched;    // coll_param.stream == nullptr
+static ccl_sched g_stream_sched;  // coll_param.stream set (never dereferenced)
 struct async_reduce_entry {
+    ccl_sched* sched;
     const void* in;
     void* inout;
     size_t cnt;
@@ -30,7 +36,7 @@ struct async_reduce_entry {
     entry_status status = not_started;
     ccl_comp_request* req = nullptr;
     void start() {
-        ccl_comp_reduce_start(in, cnt, inout, nullptr, dtype, op, nullptr, nullptr, &req);
+        ccl_comp_reduce_start(sched, in, cnt, inout, nullptr, dtype, op, nullptr, nullptr, &req);
         status = started;
         update();
     }
@@ -91,6 +97,13 @@ int main() {
     bool ok = true;
     for (size_t i = 0; i < n; i++) ok = ok && acc[i] == 1.0f;  // (P-1)*P/2 with P = 2
     EXPECT(ok, "host fp32 sum");
+    // the same entry under its schedule (no stream: host memory by its word)
+    g_stream_sched.coll_param.stream = reinterpret_cast<ccl_stream*>(&g_stream_sched);
+    st = ccl_comp_reduce(&g_host_sched, comm_buf, n, acc, nullptr, f32, ccl::reduction::sum, nullptr, &ctx);
+    EXPECT(st == ccl::status::success, "status %d", (int)st);
+    ok = true;
+    for (size_t i = 0; i < n; i++) ok = ok && acc[i] == 2.0f;
+    EXPECT(ok, "host fp32 sum under a schedule without a stream");
 
     // device buffers: reduce_local_entry with device USM (reduce_local_entry.cpp:33-58)
     float *din = nullptr, *dio = nullptr;
@@ -234,9 +247,9 @@ int main() {
         }
         std::vector<async_reduce_entry> entries;
         for (int e = 0; e < nd; e++)
-            entries.push_back({dbufs[2 * e], dbufs[2 * e + 1], m, f32, ccl::reduction::sum});
+            entries.push_back({&g_stream_sched, dbufs[2 * e], dbufs[2 * e + 1], m, f32, ccl::reduction::sum});
         for (int e = 0; e < nh; e++)
-            entries.push_back({hbufs[2 * e], hbufs[2 * e + 1], m, f32, ccl::reduction::max});
+            entries.push_back({&g_host_sched, hbufs[2 * e], hbufs[2 * e + 1], m, f32, ccl::reduction::max});
         for (auto& en : entries) en.start();
         size_t spins = 0;
         bool all = false;
@@ -271,7 +284,7 @@ int main() {
                 bx[i] = (float)(i % 89);
                 by[i] = 3.0f;
             }
-            async_reduce_entry bigen{bx, by, big, f32, ccl::reduction::sum};
+            async_reduce_entry bigen{&g_host_sched, bx, by, big, f32, ccl::reduction::sum};
             bigen.start();
             size_t sp = 0;
             while (bigen.status != complete && sp++ < 200000000) bigen.update();
@@ -282,7 +295,7 @@ int main() {
             free(by);
         }
         // empty reduce: complete at start (comp.cpp:132-134)
-        async_reduce_entry z{hbufs[0], hbufs[1], 0, f32, ccl::reduction::sum};
+        async_reduce_entry z{&g_host_sched, hbufs[0], hbufs[1], 0, f32, ccl::reduction::sum};
         z.start();
         EXPECT(z.status == complete, "empty async reduce completes at start");
         for (float* p : dbufs) (void)hipFree(p);

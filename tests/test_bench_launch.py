@@ -157,3 +157,47 @@ def test_helper_threads_take_the_process_cpu_set():
     assert r.returncode == 0, r.stderr[-2000:]
     n, total = (int(x) for x in r.stdout.split())
     assert n == total > 1
+
+
+@pytest.mark.parametrize("idents,plan", [
+    (["0:3:0/u0"], (1, 1, False)),
+    (["0:3:0/u0", "0:3:0/u0"], (1, 2, True)),         # the 2-rank rehearsal on one GPU
+    ([f"0:{b:x}:0/u{b}" for b in range(8)], (8, 1, False)),  # one rank per GPU of an 8-GPU node
+    (["a", "a", "b", "b"], (2, 2, True)),
+])
+def test_device_plan_counts_devices_not_ranks(idents, plan):
+    """n_gpus = distinct physical devices, ranks_per_device,
+    and a shared device marks the line a rehearsal."""
+    assert bench.device_plan(idents) == plan
+
+
+_GLOO_PLAN = """
+import os, sys
+sys.path.insert(0, sys.argv[1])
+import torch.distributed as dist
+import bench
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+ident = "0:3:0/shared" if r < 2 else f"0:{r:x}:0/own{r}"  # ranks 0 and 1 share a device
+idents = [None] * w
+dist.all_gather_object(idents, ident)
+n, per, reh = bench.device_plan(idents)
+peak = bench.HBM_PEAK_GBPS * n
+if r == 0:
+    print(f"PLAN {n} {per} {reh} {peak}", flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_device_plan_over_a_gloo_group(tmp_path):
+    """The plan as bench.py forms it at N > 1: every rank's identity gathered
+    over the process group (gloo here; RCCL on the node), the same on every
+    rank; 3 ranks on 2 devices -> n_gpus 2, 2 ranks per device, peak 16 TB/s."""
+    script = tmp_path / "plan.py"
+    script.write_text(_GLOO_PLAN)
+    plans = bench.rank_plan(3, [], bench.free_port(), base_env=dict(os.environ))
+    procs = [subprocess.Popen([sys.executable, str(script), str(ROOT)], env=env, stdout=subprocess.PIPE, text=True)
+             for _, env in plans]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert "PLAN 2 2 True 16000.0" in outs[0]

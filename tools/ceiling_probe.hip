@@ -1,0 +1,123 @@
+// ceiling_probe.hip — libmi_ceiling.so: memory-only probes for the measured
+// ceiling bench.py reports beside each kernel's roofline fraction
+// (roofline.ceiling_TBps / frac_of_ceiling).
+//
+// The spec peak (8 TB/s) is not reachable by any access pattern on this
+// part; what a K-input reduce can reach is bounded by how fast HBM serves
+// its K read streams and its one write stream.  So, on the reduce's own
+// buffers and in the same process:
+//   mic_read_streams  reads K streams of `bytes` each (16-byte non-temporal
+//                     loads, no arithmetic beyond an XOR that keeps the
+//                     loads alive; nothing is written unless the XOR hits a
+//                     magic value);
+//   mic_write_stream  writes one stream of `bytes` (16-byte non-temporal
+//                     stores of a constant).
+// bench.py times each over a few launch shapes, takes the fastest, and
+// prices the reduce's traffic at those rates, reads and writes sharing the
+// bus: ceiling = (K + 1) * bytes / (t_read_K + t_write).
+// Measurement infrastructure, not product: nothing in libmi_reduce calls it.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+constexpr int kMaxK = 16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct ReadArgs {
+    const u32x4* in[kMaxK];
+    uint64_t nvec;  // 16-byte vectors per stream
+    uint32_t* sink;
+};
+
+template <int K>
+__global__ void read_streams(ReadArgs a) {
+    extern __shared__ char lds_cap[];  // never touched: caps resident waves
+    (void)lds_cap;
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.nvec) return;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) x[j] = __builtin_nontemporal_load(a.in[j] + v);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) acc ^= x[j].x ^ x[j].y ^ x[j].z ^ x[j].w;
+    if (acc == 0x9E3779B9u) a.sink[v & 1023] = acc;
+}
+
+__global__ void write_stream(u32x4* out, uint64_t nvec) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nvec) return;
+    const u32x4 one = {0x3F800000u, 0x3F800000u, 0x3F800000u, 0x3F800000u};
+    __builtin_nontemporal_store(one, out + v);
+}
+
+template <int K>
+hipError_t launch_read(dim3 g, dim3 b, unsigned lds, hipStream_t s, const ReadArgs& a) {
+    hipLaunchKernelGGL(read_streams<K>, g, b, lds, s, a);
+    return hipGetLastError();
+}
+
+typedef hipError_t (*ReadFn)(dim3, dim3, unsigned, hipStream_t, const ReadArgs&);
+
+ReadFn pick(int k) {
+    switch (k) {
+        case 1: return launch_read<1>;
+        case 2: return launch_read<2>;
+        case 3: return launch_read<3>;
+        case 4: return launch_read<4>;
+        case 6: return launch_read<6>;
+        case 8: return launch_read<8>;
+        case 12: return launch_read<12>;
+        case 16: return launch_read<16>;
+        default: return nullptr;
+    }
+}
+
+// dynamic LDS per block so that `waves_per_cu` one-wave blocks fit on a CU
+// (0 = no cap); multi-wave blocks scale it by their waves
+unsigned lds_for(int block, int waves_per_cu) {
+    if (waves_per_cu <= 0) return 0;
+    int dev = 0, lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+        return 0;
+    const unsigned waves_per_block = (unsigned)((block + 63) / 64);
+    return (unsigned)lds / (unsigned)waves_per_cu * waves_per_block;
+}
+
+}  // namespace
+
+extern "C" {
+
+// 0 or the hipError_t; -1 on bad arguments.  `bytes` per stream, a multiple
+// of 16; `block` threads per block (64..1024); `waves_per_cu` 0 = uncapped.
+__attribute__((visibility("default"))) int mic_read_streams(const void* const* ptrs, int k, size_t bytes, int block,
+                                                            int waves_per_cu, void* sink, void* stream) {
+    ReadFn fn = pick(k);
+    if (!fn || !ptrs || !sink || bytes % 16 || block < 64 || block > 1024) return -1;
+    ReadArgs a{};
+    for (int j = 0; j < k; j++) a.in[j] = static_cast<const u32x4*>(ptrs[j]);
+    a.nvec = bytes / 16;
+    a.sink = static_cast<uint32_t*>(sink);
+    const uint64_t blocks = (a.nvec + (uint64_t)block - 1) / (uint64_t)block;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
+    return (int)fn(dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
+                   static_cast<hipStream_t>(stream), a);
+}
+
+__attribute__((visibility("default"))) int mic_write_stream(void* ptr, size_t bytes, int block, int waves_per_cu,
+                                                            void* stream) {
+    if (!ptr || bytes % 16 || block < 64 || block > 1024) return -1;
+    const uint64_t nvec = bytes / 16;
+    const uint64_t blocks = (nvec + (uint64_t)block - 1) / (uint64_t)block;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
+    hipLaunchKernelGGL(write_stream, dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
+                       static_cast<hipStream_t>(stream), static_cast<u32x4*>(ptr), nvec);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

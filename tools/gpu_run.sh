@@ -103,6 +103,8 @@ for step in "$@"; do
                 done
                 echo "=== smallw n=$n done" | tee -a "$OUT/steps.log"
             done ;;
+        residency)  # resident one-wave workgroups per CU against the dynamic LDS each reserves
+            run residency 120 ./tools/residency_probe 20 0 6826 6656 6144 7168 13653 13312 10240 16384 20480 27306 27136 ;;
         occk)  # the 64-lane fan-in over input count x wave cap
             run occk 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-6} 6 fank ;;
         copysweep)

@@ -76,8 +76,9 @@ int main(int argc, char** argv) {
     std::vector<double> s = us;
     std::sort(s.begin(), s.end());
     const double lk = *std::max_element(lookups.begin(), lookups.end());
-    printf("{\"mode\": \"%s\", \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
+    const char* roctx = getenv("MI_ROCTX");
+    printf("{\"mode\": \"%s%s\", \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
            "\"max_us\": %.3f, \"lookups_per_call\": %.2f, \"iters\": %ld}\n",
-           mode.c_str(), T, n, n * sizeof(float), s[T / 2], s[T - 1], lk, iters);
+           mode.c_str(), roctx && !strcmp(roctx, "0") ? " (roctx off)" : "", T, n, n * sizeof(float), s[T / 2], s[T - 1], lk, iters);
     fflush(stdout);
 }
