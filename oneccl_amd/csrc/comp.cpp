@@ -411,11 +411,15 @@ int dtype_id(const ccl_datatype& dt) { return static_cast<int>(dt.idx()); }
 
 // ---- tracing ----------------------------------------------------------------
 // The reference wraps ccl_comp_reduce_regular in an ITT event of that name
-// (comp.cpp:90-93, 116-118).  The ROCm counterpart is a roctx range, which
-// `rocprofv3 --marker-trace` records next to the kernel trace.  The roctx
+// (comp.cpp:90-93, 116-118), emitted only when CCL_ITT_LEVEL > 0
+// (sched_timer.cpp:141-203: event_get/start/end return at once at level 0,
+// the default).  The ROCm counterpart is a roctx range, which
+// `rocprofv3 --marker-trace` records next to the kernel trace, under the same
+// knob (or MI_ROCTX=1; MI_ROCTX=0 forces it off), read once.  The roctx
 // library is loaded on first use with dlopen, so the shim has no link-time
-// dependency on the profiler SDK; without it, or with MI_ROCTX=0, ranges
-// are no-ops.
+// dependency on the profiler SDK; without it ranges are no-ops.  Off, a
+// range costs nothing: on, two calls into the SDK (8 ns per 4 KiB reduce on
+// MI355X's host, profiles/round4_host/).
 struct Roctx {
     int (*push)(const char*) = nullptr;
     int (*pop)() = nullptr;
@@ -424,8 +428,10 @@ struct Roctx {
 const Roctx& roctx() {
     static const Roctx r = [] {
         Roctx x;
-        const char* off = getenv("MI_ROCTX");
-        if (off && strcmp(off, "0") == 0) return x;
+        const char* mi = getenv("MI_ROCTX");
+        const char* itt = getenv("CCL_ITT_LEVEL");
+        const bool on = mi ? strcmp(mi, "0") != 0 : (itt && atoi(itt) > 0);
+        if (!on) return x;
         for (const char* name : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
                                  "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"}) {
             void* h = dlopen(name, RTLD_NOW | RTLD_LOCAL);

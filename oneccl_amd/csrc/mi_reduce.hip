@@ -159,14 +159,18 @@ typedef hipError_t (*Launch2Fn)(dim3, hipStream_t, const R2Args&, unsigned lds);
 typedef hipError_t (*LaunchBFn)(dim3, hipStream_t, const BArgs&, unsigned lds);
 
 // Lean 2-input kernel shape: one 16-byte vector per lane, one-wave (64-lane)
-// tiles, 24 waves resident per CU (capped by idle LDS, as the fan-in below).
+// tiles, 21 waves resident per CU (capped by idle LDS, as the fan-in below).
 // In place, as ccl_comp_reduce runs it, that took 0.484 ms per GiB of fp32
 // against 0.508 for round 2's 1024-lane tiles at 32 waves per CU (-4.8 %;
 // int32 -3.5 %, bf16 -4.1 %, fp16 -3.5 %; tools/occupancy_sweep.hip r2ab,
 // profiles/round3_occupancy/).  Round 1's sweeps had stopped at 256 lanes.
+// (Round 3 sized that reservation for 24 waves; gfx950 allocates LDS in
+// granules of 1/128 of the CU's LDS, so it held 21, which is what was
+// measured: tools/residency_probe.hip, profiles/round4_host/.  The residencies
+// below are the achieved ones, and wave_cap_lds reserves whole granules.)
 constexpr int kB2 = 64;
 constexpr int kU2 = 1;
-constexpr int kLeanWavesPerCU = 24;
+constexpr int kLeanWavesPerCU = 21;
 // Buffer-addressed fan-in, one tile per block.  One-wave (64-lane) tiles,
 // with the waves resident on a CU capped by LDS that no instruction touches
 // (a block that reserves 1/W of a CU's LDS leaves room for W of them).  Each
@@ -178,7 +182,8 @@ constexpr int kLeanWavesPerCU = 24;
 // 16 inputs -7.4 %).  8- and 16-bit integers fold packed on dwords
 // (pk_op4), so no type unpacks more than 8 elements per vector.
 constexpr int kFanBlock = 64;
-int fan_waves_per_cu(int k) { return k <= 4 ? 16 : k <= 6 ? 12 : k <= 8 ? 10 : k <= 12 ? 8 : 6; }
+// (achieved residencies of round 3's caps 16 / 12 / 10 / 8 / 6, see above)
+int fan_waves_per_cu(int k) { return k <= 4 ? 16 : k <= 6 ? 11 : k <= 8 ? 9 : k <= 12 ? 8 : 5; }
 
 // LDS bytes per CU of each device (read once per device; 0 = unknown: no
 // cap).  Lock-free: every launch reads it, from any number of threads.
@@ -211,13 +216,31 @@ bool wave_cap_enabled() {
     return on;
 }
 
+// LDS is allocated to a workgroup in granules of 1/128 of a CU's LDS
+// (gfx950: 1280 B of 160 KiB; 512 B of 64 KiB on gfx942), so a workgroup
+// reserving b bytes holds ceil(b / granule) granules and a CU holds
+// floor(128 / that) such workgroups.  Measured with tools/residency_probe.hip
+// over 11 sizes (profiles/round4_host/residency_probe_run1.jsonl): 6826 B
+// (160 KiB / 24) held 21 waves, 16384 B (/ 10) held 9.  The HIP occupancy
+// API (hipOccupancyMaxActiveBlocksPerMultiprocessor) ignores the granule.
+unsigned lds_granule(unsigned per_cu) { return per_cu / 128; }
+
 // Dynamic LDS (never touched) for a one-wave block so that `waves` of them
-// fit on a CU of the device `s` launches on.
+// fit on a CU: whole granules, floor(128 / waves) of them.  Exactly `waves`
+// fit when waves is one of the residencies granules allow (floor(128 / m):
+// 32, 25, 21, 18, 16, 14, 12, 11, 10, 9, 8, ... 5, 4), as every cap here is.
+unsigned wave_cap_bytes(unsigned per_cu, int waves) {
+    if (per_cu == 0 || waves <= 0) return 0;
+    const unsigned g = lds_granule(per_cu);
+    if (g == 0) return per_cu / (unsigned)waves;
+    return std::max(1u, 128u / (unsigned)waves) * g;
+}
+
 unsigned wave_cap_lds(hipStream_t s, int waves) {
     if (!wave_cap_enabled()) return 0;
     int dev = -1;
     if (!s || hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-    return lds_per_cu(dev) / (unsigned)waves;
+    return wave_cap_bytes(lds_per_cu(dev), waves);
 }
 
 template <typename Tag, int OP, unsigned V>
@@ -1448,11 +1471,11 @@ bool needs_staging(const void* const* inputs, int k, const void* out, size_t byt
 // ---------------------------------------------------------------------------
 typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&, unsigned lds);
 
-// One-wave blocks, 24 resident per CU, as the 2-input reduce: 2^28 fp32 ->
+// One-wave blocks, 21 resident per CU (round 3's cap of 24 as allocated), as the 2-input reduce: 2^28 fp32 ->
 // bf16 0.253 -> 0.243 ms, bf16 -> fp32 0.262 -> 0.239 ms against round 2's
 // 256-lane blocks (tools/occupancy_sweep.hip copyconv, profiles/round3_occupancy/).
 constexpr int kConvBlock = 64;
-constexpr int kConvWavesPerCU = 24;
+constexpr int kConvWavesPerCU = 21;  // achieved residency of round 3's cap of 24 (see kLeanWavesPerCU)
 
 template <typename ST, typename DT, unsigned V>
 hipError_t conv_one(dim3 grid, hipStream_t s, const CArgs& a, unsigned lds) {
@@ -2177,7 +2200,7 @@ int mi_get_residency(int device, int k, int* waves_per_cu, unsigned* lds_bytes) 
     if (device < 0 && hipGetDevice(&device) != hipSuccess) device = -1;
     const int w = k == 2 ? kLeanWavesPerCU : k == 0 ? kConvWavesPerCU : fan_waves_per_cu(k);
     if (waves_per_cu) *waves_per_cu = w;
-    if (lds_bytes) *lds_bytes = wave_cap_enabled() ? lds_per_cu(device) / (unsigned)w : 0;
+    if (lds_bytes) *lds_bytes = wave_cap_enabled() ? wave_cap_bytes(lds_per_cu(device), w) : 0;
     return 0;
 }
 

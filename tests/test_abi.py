@@ -164,13 +164,13 @@ def test_version():
 
 
 def test_residency_plan():
-    """The one-wave kernels' resident-wave caps: 24 per CU for
-    the 2-input kernel and the conversions, 16/12/10/8/6 for a fan-in of
-    <=4/<=6/<=8/<=12/<=16 inputs.  Without a GPU the LDS size is unknown and
-    no cap is reserved."""
+    """The one-wave kernels' resident-wave caps, as the LDS
+    granules achieve them: 21 per CU for the 2-input kernel and the
+    conversions, 16/11/9/8/5 for a fan-in of <=4/<=6/<=8/<=12/<=16 inputs.
+    Without a GPU the LDS size is unknown and no cap is reserved."""
     m = _lib.mi()
     w, lds = ctypes.c_int(), ctypes.c_uint()
-    want = {0: 24, 1: 16, 2: 24, 3: 16, 4: 16, 5: 12, 6: 12, 7: 10, 8: 10, 9: 8, 12: 8, 13: 6, 16: 6}
+    want = {0: 21, 1: 16, 2: 21, 3: 16, 4: 16, 5: 11, 6: 11, 7: 9, 8: 9, 9: 8, 12: 8, 13: 5, 16: 5}
     for k, waves in want.items():
         assert m.mi_get_residency(-1, k, ctypes.byref(w), ctypes.byref(lds)) == 0
         assert w.value == waves, (k, w.value)

@@ -555,7 +555,8 @@ def test_comp_request_free_waits_for_pending():
 def test_roctx_range_around_reduce(tmp_path):
     """The ITT event the reference puts around ccl_comp_reduce_regular
     (comp.cpp:90-93) is a roctx range here: `rocprofv3 --marker-trace` records
-    comp_reduce_regular and comp_batch_reduce ranges from the drop-in."""
+    comp_reduce_regular and comp_batch_reduce ranges from the drop-in, under
+    the reference's own knob (CCL_ITT_LEVEL > 0; off by default, as there)."""
     import os
     import shutil
     import subprocess
@@ -575,7 +576,8 @@ def test_roctx_range_around_reduce(tmp_path):
             "comp.comp_batch_reduce(p.ctypes.data, [0, 64, 128], 64, o.ctypes.data, comp.datatype.float32, "
             "comp.reduction.sum)\n"
             "assert (b == 4).all() and (o == 3).all()\n") % str(root)
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp", CCL_ITT_LEVEL="1")
+    env.pop("MI_ROCTX", None)
     r = subprocess.run([prof, "--marker-trace", "--output-format", "csv", "-d", str(tmp_path), "-o", "trace", "--",
                         sys.executable, "-c", code], cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]

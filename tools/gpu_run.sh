@@ -103,6 +103,8 @@ for step in "$@"; do
                 done
                 echo "=== smallw n=$n done" | tee -a "$OUT/steps.log"
             done ;;
+        gran)  # the one-wave kernels at every residency whole LDS granules allow (C2, C3, C4, 6-input)
+            run gran 400 ./tools/occupancy_sweep 1024 ${SWEEP_ROUNDS:-8} 8 gran ;;
         residency)  # resident one-wave workgroups per CU against the dynamic LDS each reserves
             run residency 120 ./tools/residency_probe 20 0 6826 6656 6144 7168 13653 13312 10240 16384 20480 27306 27136 ;;
         occk)  # the 64-lane fan-in over input count x wave cap

@@ -12,7 +12,7 @@
 // runtime actually grants.  Outputs are checked bit for bit against the
 // library's default launch before timing.
 //
-//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|fanu|xcd|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops]   (all = c2, c3, c4)
+//   occupancy_sweep [bucket_MiB=1024] [rounds=6] [reps=8] [c2|c3|c4|all|c4bf|fank|fanu|xcd|r2ab|copyconv|pmcset|r2u|copyu|policy|c5ops|gran]   (all = c2, c3, c4)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -291,6 +291,41 @@ void add_fan(std::vector<Variant>& vs, const char* group, KArgs a, size_t bytes,
                   }, a.out, ref, bytes, {}});
 }
 
+// gfx950 allocates LDS in granules of LDS-per-CU / 128 (1280 B of 160 KiB):
+// a workgroup reserving `lds` bytes holds ceil(lds / granule) of them, so a
+// CU holds 128 / that many one-wave workgroups (tools/residency_probe.hip
+// measured it; hipOccupancyMaxActiveBlocksPerMultiprocessor ignores the
+// granule).  The one-wave kernels at an exact granule count m: residency
+// floor(128 / m), `gran` mode.
+constexpr unsigned kGranule = kLdsPerCU / 128;
+int resident_of(unsigned lds) { return lds ? (int)std::min(32u, 128u / ((lds + kGranule - 1) / kGranule)) : 32; }
+
+template <typename Tag, unsigned V, int OPX = OP_SUM>
+void add_r2_granules(std::vector<Variant>& vs, const char* group, R2Args r, size_t bytes, unsigned m) {
+    const unsigned blocks = (unsigned)(r.nvec / 64);
+    const unsigned lds = m * kGranule;
+    char name[200];
+    snprintf(name, sizeof name, "%s reduce2_kernel 64x1, lds %u B = %u granules -> %d waves per CU (measured rule)",
+             group, lds, m, resident_of(lds));
+    vs.push_back({name, group, 3.0 * bytes, [r, blocks, lds](hipStream_t s) {
+                      hipLaunchKernelGGL((reduce2_kernel<Tag, OPX, V, 1, 64>), dim3(blocks), dim3(64), lds, s, r);
+                      return hipGetLastError();
+                  }, r.out, nullptr, bytes, {}});
+}
+
+template <typename Tag, unsigned V>
+void add_fan_granules(std::vector<Variant>& vs, const char* group, KArgs a, size_t bytes, unsigned m) {
+    const unsigned blocks = (unsigned)(a.nvec / 64);
+    const unsigned lds = m * kGranule;
+    char name[200];
+    snprintf(name, sizeof name, "%s fan_kernel 64x1, lds %u B = %u granules -> %d waves per CU (measured rule)", group,
+             lds, m, resident_of(lds));
+    vs.push_back({name, group, (a.k + 1.0) * bytes, [a, blocks, lds](hipStream_t s) {
+                      hipLaunchKernelGGL((fan_kernel<Tag, OP_SUM, V, 64, 8>), dim3(blocks), dim3(64), lds, s, a);
+                      return hipGetLastError();
+                  }, a.out, nullptr, bytes, {}});
+}
+
 // every block size at every cap (caps a block size cannot meet are skipped)
 constexpr int kCaps[] = {0, 24, 20, 16, 12, 8, 6, 4};
 
@@ -422,6 +457,38 @@ int main(int argc, char** argv) {
         rb.trunc_from = bytes3 / 2;
         shapes(bf16_tag(), std::integral_constant<unsigned, V_BF16_RNE>(), "C3 bf16 sum 256 MiB in place:", rb, bytes3);
         shapes(fp16_tag(), std::integral_constant<unsigned, 0u>(), "C3 fp16 sum 256 MiB in place:", rb, bytes3);
+    }
+    if (which == "gran") {
+        // exact residencies (whole LDS granules): the 2-input kernel in place
+        // (fp32, bf16) and the fan-in (8 and 6 inputs), every residency the
+        // granules allow from 32 down
+        R2Args r{};
+        r.acc = r.out = buf[0];
+        r.in = buf[1];
+        r.nvec = bytes / 16;
+        r.trunc_from = bytes / 4;
+        for (unsigned m : {0u, 4u, 5u, 6u, 7u, 8u})
+            add_r2_granules<float, 0u>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, m);
+        R2Args rb{};
+        rb.acc = rb.out = buf[2];
+        rb.in = buf[3];
+        rb.nvec = bytes3 / 16;
+        rb.trunc_from = bytes3 / 2;
+        for (unsigned m : {0u, 5u, 6u, 7u})
+            add_r2_granules<bf16_tag, V_BF16_RNE>(vs, "C3 bf16 sum 256 MiB in place:", rb, bytes3, m);
+        KArgs a{};
+        for (int i = 0; i < 8; i++) a.in[i] = buf[i];
+        a.out = buf[8];
+        a.k = 8;
+        a.count = bytes / 4;
+        a.nvec = bytes / 16;
+        a.trunc_from = a.count;
+        for (unsigned m : {8u, 9u, 10u, 11u, 12u, 13u, 15u, 16u, 18u})
+            add_fan_granules<float, 0u>(vs, "C4 fp32 8-input 1 GiB:", a, bytes, m);
+        KArgs a6 = a;
+        a6.k = 6;
+        for (unsigned m : {8u, 9u, 10u, 11u, 12u, 13u, 16u})
+            add_fan_granules<float, 0u>(vs, "fan-in fp32 6-input 1 GiB:", a6, bytes, m);
     }
     if (which == "c5ops") {
         // the library's 2-input launch over dtypes and ops, same buffers, in place

@@ -76,9 +76,12 @@ int main(int argc, char** argv) {
     std::vector<double> s = us;
     std::sort(s.begin(), s.end());
     const double lk = *std::max_element(lookups.begin(), lookups.end());
-    const char* roctx = getenv("MI_ROCTX");
+    // roctx ranges are on only under CCL_ITT_LEVEL > 0 or MI_ROCTX=1 (comp.cpp)
+    const char* mi = getenv("MI_ROCTX");
+    const char* itt = getenv("CCL_ITT_LEVEL");
+    const bool roctx_on = mi ? strcmp(mi, "0") != 0 : (itt && atoi(itt) > 0);
     printf("{\"mode\": \"%s%s\", \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
            "\"max_us\": %.3f, \"lookups_per_call\": %.2f, \"iters\": %ld}\n",
-           mode.c_str(), roctx && !strcmp(roctx, "0") ? " (roctx off)" : "", T, n, n * sizeof(float), s[T / 2], s[T - 1], lk, iters);
+           mode.c_str(), roctx_on ? " (roctx on)" : "", T, n, n * sizeof(float), s[T / 2], s[T - 1], lk, iters);
     fflush(stdout);
 }
