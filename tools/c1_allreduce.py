@@ -64,7 +64,7 @@ def nreduce_allreduce(buf, rank, world, reduce2, recv_bufs, fused=None):
     return t_red
 
 
-def worker(rank, world, port, count, iters, mode, q, fused_call=False):
+def worker(rank, world, port, count, iters, mode, q, fused_call=False, sched=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if mode == "dropin-gpu":  # the drop-in with its CPU path off: every reduce on the GPU
         os.environ["CCL_COMP_HOST_MAX_BYTES"] = "0"
@@ -74,7 +74,9 @@ def worker(rank, world, port, count, iters, mode, q, fused_call=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         if mode in ("dropin", "dropin-gpu"):
-            from oneccl_amd import comp
+            from oneccl_amd import _lib, comp
+            if sched:  # the entries' schedule, as a CPU oneCCL build passes it: no stream, host memory
+                _lib.shim().mi_ccl_comp_shim_sched(1)
 
             def reduce2(inp, inout):
                 comp.comp_reduce(inp.data_ptr(), inp.numel(), inout.data_ptr(), comp.datatype.float32,
@@ -124,7 +126,7 @@ def worker(rank, world, port, count, iters, mode, q, fused_call=False):
         dist.destroy_process_group()
 
 
-def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False):
+def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False, sched=False):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -132,7 +134,7 @@ def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, world, port, count, iters, mode, q, fused_call))
+    procs = [ctx.Process(target=worker, args=(r, world, port, count, iters, mode, q, fused_call, sched))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -141,6 +143,7 @@ def run(world=2, count=262144, iters=50, mode="dropin", fused_call=False):
         p.join(timeout=60)
     return {"config": "examples/benchmark allreduce fp32 sum, loopback (BASELINE configs[0])", "ranks": world,
             "count": count, "bytes": count * 4, "local_reduce": mode, "fused_batch_reduce": fused_call,
+            "host_schedule": sched,
             "iters": iters,
             "correct": all(r[1] for r in res) and all(p.exitcode == 0 for p in procs),
             "best_us": round(res[0][2][0] * 1e6, 1), "median_us": round(res[0][2][1] * 1e6, 1),
@@ -158,5 +161,7 @@ if __name__ == "__main__":
                     help="dropin: the shim with its default dispatch (small host chunks on the CPU); "
                          "dropin-gpu: the shim with every reduce on the GPU; oracle: the CPU restatement")
     ap.add_argument("--fused", action="store_true", help="one ccl_comp_batch_reduce per rank")
+    ap.add_argument("--sched", action="store_true",
+                    help="pass a schedule without a stream, as the entries of a CPU oneCCL build do (no lookups)")
     a = ap.parse_args()
-    print(json.dumps(run(a.ranks, a.count, a.iters, a.reduce, a.fused)), flush=True)
+    print(json.dumps(run(a.ranks, a.count, a.iters, a.reduce, a.fused, a.sched)), flush=True)

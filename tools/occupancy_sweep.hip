@@ -469,12 +469,23 @@ int main(int argc, char** argv) {
         r.trunc_from = bytes / 4;
         for (unsigned m : {0u, 4u, 5u, 6u, 7u, 8u})
             add_r2_granules<float, 0u>(vs, "C2 fp32 sum 1 GiB in place:", r, bytes, m);
+        // bf16 operands of their own, every half a finite bf16 (as r2ab fills
+        // them): random bits would make NaN/Inf halves common and send rows
+        // through the x86 NaN refold
+        void *la, *lb;
+        CK(hipMalloc(&la, bytes3));
+        CK(hipMalloc(&lb, bytes3));
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)la, bytes3 / 4, 0x1234u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, s, (uint32_t*)lb, bytes3 / 4, 0x4321u, 0x3FFF3FFFu,
+                           0x3C003C00u);
+        CK(hipStreamSynchronize(s));
         R2Args rb{};
-        rb.acc = rb.out = buf[2];
-        rb.in = buf[3];
+        rb.acc = rb.out = la;
+        rb.in = lb;
         rb.nvec = bytes3 / 16;
         rb.trunc_from = bytes3 / 2;
-        for (unsigned m : {0u, 5u, 6u, 7u})
+        for (unsigned m : {0u, 5u, 6u, 7u, 8u})
             add_r2_granules<bf16_tag, V_BF16_RNE>(vs, "C3 bf16 sum 256 MiB in place:", rb, bytes3, m);
         KArgs a{};
         for (int i = 0; i < 8; i++) a.in[i] = buf[i];
