@@ -329,8 +329,9 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
         return None
     L = ctypes.CDLL(str(path))
     L.mic_read_streams.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
-                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    L.mic_write_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.mic_write_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p]
     from oneccl_amd import _lib
     waves = ctypes.c_int(0)
     _lib.check(_lib.mi().mi_get_residency(-1, k, ctypes.byref(waves), None), "mi_get_residency")
@@ -340,33 +341,36 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
     sh = stream.cuda_stream
     nb = nbytes - nbytes % 16
 
-    def best(launch):
+    def best(launch, flavors):
         res = []
-        for block, w in shapes:
-            for _ in range(2):
-                if launch(block, w):
-                    break
-            else:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(launches):
-                    launch(block, w)
-                e1.record(stream)
-                torch.cuda.synchronize()
-                res.append((e0.elapsed_time(e1) / launches, block, w))
+        for fl in flavors:
+            for block, w in shapes:
+                for _ in range(2):
+                    if launch(block, w, fl):
+                        break
+                else:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(launches):
+                        launch(block, w, fl)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    res.append((e0.elapsed_time(e1) / launches, block, w, fl))
         return min(res) if res else None
 
-    r = best(lambda b, w: L.mic_read_streams(arr, k, nb, b, w, sink.data_ptr(), sh))
-    wr = best(lambda b, w: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, sh))
+    r = best(lambda b, w, fl: L.mic_read_streams(arr, k, nb, b, w, fl, sink.data_ptr(), sh), (0, 1))
+    wr = best(lambda b, w, fl: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, fl, sh), (0, 1, 2))
     if not r or not wr:
         return None
     t = (r[0] + wr[0]) / 1e3
+    flav = {0: "global nt", 1: "buffer nt", 2: "buffer sc1 nt"}
     return {"ceiling_TBps": round((k + 1) * nb / t / 1e12, 3),
-            "read_TBps": round(k * nb / (r[0] / 1e3) / 1e12, 3), "read_shape": [r[1], r[2]],
-            "write_TBps": round(nb / (wr[0] / 1e3) / 1e12, 3), "write_shape": [wr[1], wr[2]],
+            "read_TBps": round(k * nb / (r[0] / 1e3) / 1e12, 3), "read_shape": [r[1], r[2], flav[r[3]]],
+            "write_TBps": round(nb / (wr[0] / 1e3) / 1e12, 3), "write_shape": [wr[1], wr[2], flav[wr[3]]],
             "method": f"memory-only probes on this leg's buffers (tools/ceiling_probe.hip): {k} read streams and one "
-                      "write stream, each timed alone over block x wave-cap shapes [block, waves/CU (0 = no cap)], "
-                      "best shape; ceiling = (k+1) x bytes / (t_read + t_write)"}
+                      "write stream, each timed alone over block x wave-cap shapes and the load/store flavours the "
+                      "kernels use [block, waves/CU (0 = no cap), flavour], best taken; ceiling = (k+1) x bytes / "
+                      "(t_read + t_write)"}
 
 
 def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None,

@@ -227,3 +227,42 @@ def test_readers_never_see_a_freed_snapshot():
         t.join()
     assert m.mi_host_undeclare(hp) == 0
     assert errors == []
+
+
+def test_more_reader_threads_than_slots():
+    """Past 256 concurrent reader threads the rest read under the writers'
+    lock instead of a slot; every thread still gets the declared kind, and
+    exited threads give their slots back."""
+    m = _lib.mi()
+    buf = np.zeros(1 << 12, np.uint8)
+    assert m.mi_host_declare(buf.ctypes.data, buf.nbytes) == 0
+    start = threading.Barrier(300)
+    hold = threading.Event()
+    bad = []
+
+    def reader():
+        start.wait()
+        if m.mi_host_declared_kind(buf.ctypes.data + 64, 64) != 2:
+            bad.append(1)
+        hold.wait(30)  # keep the slot taken while the others read
+        if m.mi_host_declared_kind(buf.ctypes.data, 16) != 2:
+            bad.append(2)
+
+    ts = [threading.Thread(target=reader) for _ in range(300)]
+    for t in ts:
+        t.start()
+    # a writer publishing while 300 readers hold their thread state
+    other = np.zeros(64, np.uint8)
+    assert m.mi_host_declare(other.ctypes.data, other.nbytes) == 0
+    assert m.mi_host_undeclare(other.ctypes.data) == 0
+    hold.set()
+    for t in ts:
+        t.join()
+    assert bad == []
+    # slots came back: new threads read through slots again (and still see the range)
+    res = []
+    t = threading.Thread(target=lambda: res.append(m.mi_host_declared_kind(buf.ctypes.data, 16)))
+    t.start()
+    t.join()
+    assert res == [2]
+    assert m.mi_host_undeclare(buf.ctypes.data) == 0

@@ -10,9 +10,13 @@
 //                     loads, no arithmetic beyond an XOR that keeps the
 //                     loads alive; nothing is written unless the XOR hits a
 //                     magic value);
-//   mic_write_stream  writes one stream of `bytes` (16-byte non-temporal
-//                     stores of a constant).
-// bench.py times each over a few launch shapes, takes the fastest, and
+//   mic_write_stream  writes one stream of `bytes` (16-byte stores of a
+//                     constant).
+// Each in the instruction flavours the library's kernels use (`flavor`):
+// 0 = global_load/store ... nt; 1 = buffer_load/store ... nt through a
+// per-workgroup descriptor; 2 (stores) = buffer_store ... sc1 nt, which the
+// 2-input kernel uses (the line leaves L2 as it is written).
+// bench.py times each over a few launch shapes and flavours, takes the fastest, and
 // prices the reduce's traffic at those rates, reads and writes sharing the
 // bus: ceiling = (K + 1) * bytes / (t_read_K + t_write).
 // Measurement infrastructure, not product: nothing in libmi_reduce calls it.
@@ -30,6 +34,41 @@ struct ReadArgs {
     uint64_t nvec;  // 16-byte vectors per stream
     uint32_t* sink;
 };
+
+constexpr int kAuxNT = 2, kAuxSC1NT = 18;  // buffer op aux bits (gfx950), as reduce_kernels.hpp
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(const void* base, uint64_t nvec) {
+    const uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t left = nvec - v0;
+    const uint32_t bytes = (uint32_t)(left < blockDim.x ? left : blockDim.x) * 16u;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(base)) + v0 * 16, (short)0,
+                                             (int)bytes, 0x00020000);
+}
+
+template <int K>
+__global__ void read_streams_buf(ReadArgs a) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    if ((uint64_t)blockIdx.x * blockDim.x >= a.nvec) return;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; j++)
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(block_rsrc(a.in[j], a.nvec), threadIdx.x * 16u, 0, kAuxNT);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) acc ^= x[j].x ^ x[j].y ^ x[j].z ^ x[j].w;
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (acc == 0x9E3779B9u && v < a.nvec) a.sink[v & 1023] = acc;
+}
+
+template <int AUX>
+__global__ void write_stream_buf(u32x4* out, uint64_t nvec) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    if ((uint64_t)blockIdx.x * blockDim.x >= nvec) return;
+    const u32x4 one = {0x3F800000u, 0x3F800000u, 0x3F800000u, 0x3F800000u};
+    __builtin_amdgcn_raw_buffer_store_b128(one, block_rsrc(out, nvec), threadIdx.x * 16u, 0, AUX);
+}
 
 template <int K>
 __global__ void read_streams(ReadArgs a) {
@@ -55,38 +94,45 @@ __global__ void write_stream(u32x4* out, uint64_t nvec) {
     __builtin_nontemporal_store(one, out + v);
 }
 
-template <int K>
+template <int K, bool BUF>
 hipError_t launch_read(dim3 g, dim3 b, unsigned lds, hipStream_t s, const ReadArgs& a) {
-    hipLaunchKernelGGL(read_streams<K>, g, b, lds, s, a);
+    if (BUF)
+        hipLaunchKernelGGL(read_streams_buf<K>, g, b, lds, s, a);
+    else
+        hipLaunchKernelGGL(read_streams<K>, g, b, lds, s, a);
     return hipGetLastError();
 }
 
 typedef hipError_t (*ReadFn)(dim3, dim3, unsigned, hipStream_t, const ReadArgs&);
 
-ReadFn pick(int k) {
+template <bool BUF>
+ReadFn pick_k(int k) {
     switch (k) {
-        case 1: return launch_read<1>;
-        case 2: return launch_read<2>;
-        case 3: return launch_read<3>;
-        case 4: return launch_read<4>;
-        case 6: return launch_read<6>;
-        case 8: return launch_read<8>;
-        case 12: return launch_read<12>;
-        case 16: return launch_read<16>;
+        case 1: return launch_read<1, BUF>;
+        case 2: return launch_read<2, BUF>;
+        case 3: return launch_read<3, BUF>;
+        case 4: return launch_read<4, BUF>;
+        case 6: return launch_read<6, BUF>;
+        case 8: return launch_read<8, BUF>;
+        case 12: return launch_read<12, BUF>;
+        case 16: return launch_read<16, BUF>;
         default: return nullptr;
     }
 }
 
+ReadFn pick(int k, int flavor) { return flavor == 0 ? pick_k<false>(k) : flavor == 1 ? pick_k<true>(k) : nullptr; }
+
 // dynamic LDS per block so that `waves_per_cu` one-wave blocks fit on a CU
-// (0 = no cap); multi-wave blocks scale it by their waves
+// (0 = no cap), in whole granules of 1/128 of the CU's LDS as the library
+// reserves it (mi_reduce.hip wave_cap_bytes); one-wave blocks only
 unsigned lds_for(int block, int waves_per_cu) {
-    if (waves_per_cu <= 0) return 0;
+    if (waves_per_cu <= 0 || block != 64) return 0;
     int dev = 0, lds = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || lds <= 0)
         return 0;
-    const unsigned waves_per_block = (unsigned)((block + 63) / 64);
-    return (unsigned)lds / (unsigned)waves_per_cu * waves_per_block;
+    const unsigned g = (unsigned)lds / 128u;
+    return (128u / (unsigned)waves_per_cu) * g;
 }
 
 }  // namespace
@@ -94,10 +140,11 @@ unsigned lds_for(int block, int waves_per_cu) {
 extern "C" {
 
 // 0 or the hipError_t; -1 on bad arguments.  `bytes` per stream, a multiple
-// of 16; `block` threads per block (64..1024); `waves_per_cu` 0 = uncapped.
+// of 16; `block` threads per block (64..1024); `waves_per_cu` 0 = uncapped;
+// `flavor` as above (reads: 0, 1).
 __attribute__((visibility("default"))) int mic_read_streams(const void* const* ptrs, int k, size_t bytes, int block,
-                                                            int waves_per_cu, void* sink, void* stream) {
-    ReadFn fn = pick(k);
+                                                            int waves_per_cu, int flavor, void* sink, void* stream) {
+    ReadFn fn = pick(k, flavor);
     if (!fn || !ptrs || !sink || bytes % 16 || block < 64 || block > 1024) return -1;
     ReadArgs a{};
     for (int j = 0; j < k; j++) a.in[j] = static_cast<const u32x4*>(ptrs[j]);
@@ -110,13 +157,21 @@ __attribute__((visibility("default"))) int mic_read_streams(const void* const* p
 }
 
 __attribute__((visibility("default"))) int mic_write_stream(void* ptr, size_t bytes, int block, int waves_per_cu,
-                                                            void* stream) {
-    if (!ptr || bytes % 16 || block < 64 || block > 1024) return -1;
+                                                            int flavor, void* stream) {
+    if (!ptr || bytes % 16 || block < 64 || block > 1024 || flavor < 0 || flavor > 2) return -1;
     const uint64_t nvec = bytes / 16;
     const uint64_t blocks = (nvec + (uint64_t)block - 1) / (uint64_t)block;
     if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
-    hipLaunchKernelGGL(write_stream, dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
-                       static_cast<hipStream_t>(stream), static_cast<u32x4*>(ptr), nvec);
+    const dim3 g((unsigned)blocks), b((unsigned)block);
+    const unsigned lds = lds_for(block, waves_per_cu);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    u32x4* out = static_cast<u32x4*>(ptr);
+    if (flavor == 0)
+        hipLaunchKernelGGL(write_stream, g, b, lds, s, out, nvec);
+    else if (flavor == 1)
+        hipLaunchKernelGGL(write_stream_buf<kAuxNT>, g, b, lds, s, out, nvec);
+    else
+        hipLaunchKernelGGL(write_stream_buf<kAuxSC1NT>, g, b, lds, s, out, nvec);
     return (int)hipGetLastError();
 }
 
