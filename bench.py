@@ -573,12 +573,17 @@ def launch_ranks(plans, timeout=None):
 
 
 def device_identity(index):
-    """A physical device's identity: PCI domain:bus:device and UUID when the
-    runtime reports them (ranks on one GPU share it)."""
+    """A physical device's identity: PCI domain:bus:device and UUID (ranks on
+    one GPU share it).  Should the runtime report neither, the identity falls
+    back to the visible device index within this node's visible set, so
+    ranks on different GPUs never merge into one device."""
     import torch
     p = torch.cuda.get_device_properties(index)
-    pci = ":".join(f"{getattr(p, a, -1):x}" for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
-    return f"{pci}/{getattr(p, 'uuid', '')}"
+    ids = [getattr(p, a, -1) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    uuid = str(getattr(p, "uuid", "") or "")
+    if all(v in (-1, 0) for v in ids) and uuid.strip("0-") == "":
+        return f"visible:{os.environ.get('HIP_VISIBLE_DEVICES', os.environ.get('CUDA_VISIBLE_DEVICES', '*'))}:{index}"
+    return ":".join(f"{v:x}" for v in ids) + f"/{uuid}"
 
 
 def device_plan(idents):
@@ -748,6 +753,7 @@ def main():
             "n_gpus": n_devices,
             "ranks": pg_world,
             "ranks_per_device": ranks_per_device,
+            "devices": sorted(set(idents)),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
