@@ -496,7 +496,6 @@ int pointer_kind(const void* p, size_t bytes) {
     return mi_pointer_kind_range(p, bytes, &dev);
 }
 
-
 // Each distinct pointer is classified once: the lookup
 // (hipPointerGetAttributes) takes a runtime-wide lock, so with several worker
 // threads reducing small host chunks it is the one step that serialises
