@@ -201,3 +201,21 @@ def test_device_plan_over_a_gloo_group(tmp_path):
     outs = [p.communicate(timeout=120)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs)
     assert "PLAN 2 2 True 16000.0" in outs[0]
+
+
+def test_device_identity_uses_pci_and_uuid_and_falls_back(monkeypatch):
+    """Distinct GPUs must never merge into one device in the N-rank line: PCI
+    ids and UUID when the runtime reports them, else the visible index."""
+    import types
+
+    import torch
+    props = {0: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x11, pci_device_id=0, uuid="abc"),
+             1: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x2f, pci_device_id=0, uuid="def"),
+             2: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0, pci_device_id=0, uuid=""),
+             3: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0, pci_device_id=0, uuid="")}
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props[i])
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    ids = [bench.device_identity(i) for i in range(4)]
+    assert ids[0] == "0:11:0/abc" and ids[1] == "0:2f:0/def"
+    assert ids[2] != ids[3] and ids[2].startswith("visible:")
+    assert bench.device_plan(ids) == (4, 1, False)
