@@ -46,6 +46,9 @@ int mi_ccl_comp_batch_reduce_custom(const void* in_buf, const size_t* offsets, s
                                     int bf16_keep_precision_mode, mi_ccl_reduction_fn fn);
 /* ccl_comp_copy, src/comp/comp.cpp:60-74 */
 int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal);
+/* ccl_comp_copy_host (mi_ccl_comp_async.hpp): a copy its caller knows to be
+ * host to host, with no pointer lookup */
+int mi_ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal);
 /* ccl_bf16_reduce, src/comp/bf16/bf16.cpp:87-110 (MPI user-op entry,
  * src/atl/mpi/atl_mpi_ctx.cpp:87-92) */
 int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);

@@ -1,6 +1,7 @@
 /*
  * mi_ccl_comp_async.hpp — asynchronous form of oneCCL's ccl_comp_reduce
- * (SURVEY.md §8f rank 4), defined by the drop-in shim oneccl_amd/csrc/comp.cpp.
+ * (SURVEY.md §8f rank 4), and the host copy of the copy entries, defined by
+ * the drop-in shim oneccl_amd/csrc/comp.cpp for the patched schedule entries.
  *
  * The reference's call is synchronous: reduce_local_entry::start_on_host()
  * (src/sched/entry/reduce_local_entry.cpp:98-114) and
@@ -65,5 +66,13 @@ void ccl_comp_request_wait(ccl_comp_request* req);
 
 /* Release a request (call after it tested complete, or after wait). */
 void ccl_comp_request_free(ccl_comp_request* req);
+
+/* ccl_comp_copy for a copy the caller knows to be host to host: the
+ * regular copy of copy_entry (src/sched/entry/copy/copy_entry.cpp:201-206)
+ * and recv_copy_entry's (recv_copy_entry.cpp:53), the only callers of
+ * ccl_comp_copy in the tree, both on host memory by construction.  The
+ * reference's memcpy / non-temporal copy (comp.cpp:60-74) on the calling
+ * thread, no pointer classified (integration/0006).  Errors throw.        */
+ccl::status ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, bool use_nontemporal);
 
 #endif

@@ -97,6 +97,7 @@ SHIM_API = [
     ("mi_ccl_comp_batch_reduce_custom", c_int, [c_void_p, POINTER(c_size_t), c_size_t, c_size_t, c_void_p,
                                                 POINTER(c_size_t), c_int, c_int, MI_CCL_REDUCTION_FN]),
     ("mi_ccl_comp_copy", c_int, [c_void_p, c_void_p, c_size_t, c_int]),
+    ("mi_ccl_comp_copy_host", c_int, [c_void_p, c_void_p, c_size_t, c_int]),
     ("mi_ccl_bf16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
     ("mi_ccl_fp16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
     ("mi_ccl_convert_fp32_to_bf16_arrays", c_int, [c_void_p, c_void_p, c_size_t]),

@@ -918,6 +918,25 @@ ccl::status ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, bool 
     return ccl::status::success;
 }
 
+// The copy of a regular (host) copy entry: oneCCL calls ccl_comp_copy only
+// there (copy_entry.cpp:201-206, whose copy type is `regular` only without a
+// stream or for h2h, and which asserts neither buffer is device USM, :90-97;
+// recv_copy_entry.cpp:53 with an h2h attribute, allreduce.cpp:396-422).  So
+// the patched entries (integration/0006) say so and no pointer is looked up:
+// the reference's memcpy / non-temporal memcpy (comp.cpp:60-74,
+// common/utils/memcpy.hpp) on the calling thread, after its own asynchronous
+// requests.
+ccl::status ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, bool use_nontemporal) {
+    if (bytes == 0) return ccl::status::success;
+    if (!in_buf) MI_CCL_THROW("in_buf is null");
+    if (!out_buf) MI_CCL_THROW("out_buf is null");
+    MI_LOG_DEBUG("copy: bytes ", bytes, ", operands: host memory by the copy entry (not looked up), path: cpu",
+                 use_nontemporal ? " (non-temporal)" : "");
+    check(mi_thread_sync(), "mi_thread_sync");
+    check(mi_host_copy(out_buf, in_buf, bytes, use_nontemporal ? 1 : 0), "mi_host_copy");
+    return ccl::status::success;
+}
+
 void ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
     if (out_cnt != nullptr) *out_cnt = in_cnt;
     if (!builtin_op(op)) MI_CCL_FATAL(unexpected(static_cast<int>(op)));  // bf16.cpp:73, bf16_intrisics.hpp:131
@@ -1327,6 +1346,10 @@ int mi_ccl_comp_batch_reduce_custom(const void* in_buf, const size_t* offsets, s
 
 int mi_ccl_comp_copy(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal) {
     MI_SHIM_GUARD(return (int)ccl_comp_copy(in_buf, out_buf, bytes, use_nontemporal != 0));
+}
+
+int mi_ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, int use_nontemporal) {
+    MI_SHIM_GUARD(return (int)ccl_comp_copy_host(in_buf, out_buf, bytes, use_nontemporal != 0));
 }
 
 int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {

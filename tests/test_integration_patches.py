@@ -15,7 +15,8 @@ reference tree is only read.  Runs where /root/reference exists.
   0002  atl_mpi_ctx.cpp           MPI fp16 user op through ccl_fp16_reduce          (§2b)
   0003  reduce_local_entry, recv_reduce_entry: start the reduce, poll it        (§2d)
   0004  allreduce.cpp nreduce + entry_factory.hpp: one fused fan-in per segment (§2e)
-  0005  buffer_cache.cpp: the regular buffer cache declares its host buffers     (§2f)
+  0005  buffer_cache.cpp: the regular buffer cache declares its host buffers     (§2h)
+  0006  copy_entry.cpp, recv_copy_entry.cpp: host copies say so (no lookup)      (§2i)
 """
 from __future__ import annotations
 
@@ -42,6 +43,8 @@ UNITS = {  # translation units the patches touch (headers through their includer
     "allreduce": "src/coll/algorithms/allreduce/allreduce.cpp",  # recv_reduce_entry.hpp, entry_factory.hpp
     "atl_mpi_ctx": "src/atl/mpi/atl_mpi_ctx.cpp",
     "buffer_cache": "src/sched/buffer/buffer_cache.cpp",
+    "copy_entry": "src/sched/entry/copy/copy_entry.cpp",
+    "recv_copy_entry": "src/sched/entry/recv_copy_entry.cpp",
 }
 
 
@@ -88,7 +91,7 @@ def test_patch_set_is_complete():
     names = [p.name for p in PATCHES]
     assert names == ["0001-build-swap-src-comp.patch", "0002-atl-mpi-fp16-user-op.patch",
                      "0003-async-host-reduce-entries.patch", "0004-nreduce-fused-fanin.patch",
-                     "0005-buffer-cache-declares-host-buffers.patch"], names
+                     "0005-buffer-cache-declares-host-buffers.patch", "0006-copy-entries-host-copy.patch"], names
     assert (NEW_FILES / "sched" / "entry" / "batch_reduce_entry.hpp").exists()
 
 
@@ -123,6 +126,10 @@ def test_patched_units_need_only_what_the_dropin_defines(objs):
     drop-in's in-tree object."""
     ours = _global_defs(objs["ours"][0])
     comp_api = re.compile(r"ccl_comp_|ccl_fp16_reduce|ccl_bf16_reduce|ccl_reduction_to_str")
+    for name in ("copy_entry", "recv_copy_entry"):  # 0006: the host copy, not the classifying one
+        need = _undefs(objs[name][0])
+        assert any("ccl_comp_copy_host" in x for x in need), name
+        assert not any(re.search(r"ccl_comp_copyPKv", x) for x in need), name
     for name in UNITS:
         need = {s for s in _undefs(objs[name][0]) if comp_api.search(s)}
         missing = sorted(need - ours)

@@ -161,3 +161,33 @@ def test_host_schedule_under_concurrent_workers(shim):
     for w in ws:
         w.join()
     assert errors == []
+
+
+@pytest.mark.parametrize("nbytes", [1, 255, 4096, 65536 + 7, 1 << 20])
+@pytest.mark.parametrize("nt", [0, 1])
+def test_copy_entries_host_copy_makes_no_lookup(shim, nbytes, nt):
+    """ccl_comp_copy_host (integration/0006): the regular copy of copy_entry
+    and recv_copy_entry's copy, host to host by construction
+    (copy_entry.cpp:90-97, allreduce.cpp:396-422), copy bytes exactly with no
+    pointer lookup; ccl_comp_copy itself still classifies (2 lookups)."""
+    rng = np.random.default_rng(nbytes)
+    src = rng.integers(0, 256, nbytes + 64, dtype=np.uint8)
+    dst = np.zeros(nbytes + 64, np.uint8)
+    n0 = shim.mi_ccl_comp_pointer_lookups()
+    _lib.check_shim(shim.mi_ccl_comp_copy_host(src.ctypes.data + 3, dst.ctypes.data + 5, nbytes, nt), "copy_host")
+    assert shim.mi_ccl_comp_pointer_lookups() == n0
+    assert np.array_equal(dst[5:5 + nbytes], src[3:3 + nbytes])
+    assert not dst[:5].any() and not dst[5 + nbytes:].any()
+    dst[:] = 0
+    n0 = shim.mi_ccl_comp_pointer_lookups()
+    _lib.check_shim(shim.mi_ccl_comp_copy(src.ctypes.data, dst.ctypes.data, nbytes, nt), "copy")
+    assert shim.mi_ccl_comp_pointer_lookups() - n0 == 2
+    assert np.array_equal(dst[:nbytes], src[:nbytes])
+
+
+def test_copy_host_argument_errors(shim):
+    a = np.zeros(16, np.uint8)
+    assert shim.mi_ccl_comp_copy_host(None, a.ctypes.data, 16, 0) == -1
+    assert b"in_buf is null" in shim.mi_ccl_last_error()
+    assert shim.mi_ccl_comp_copy_host(a.ctypes.data, None, 16, 0) == -1
+    assert shim.mi_ccl_comp_copy_host(None, None, 0, 0) == 0  # empty: nothing checked, as ccl_comp_copy

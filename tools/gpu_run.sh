@@ -95,7 +95,7 @@ for step in "$@"; do
                  # schedule) against the reference's own compiled CPU loop, one JSON line each
             for n in ${SMALLW_ELEMS:-1024 16384 131072}; do
                 for T in 1 2 4 8 16; do
-                    for mode in ${SMALLW_MODES:-default reg sched ref}; do
+                    for mode in ${SMALLW_MODES:-default reg sched ref copy copyhost memcpy}; do
                         timeout -k 10 120 ./tools/small_workers $T $n $mode >> "$OUT/smallw.jsonl" 2>> "$OUT/smallw.err"
                         rc=$?
                         [ $rc -eq 0 ] || { echo "STOP: smallw $T $n $mode rc=$rc" | tee -a "$OUT/steps.log"; exit $rc; }

@@ -11,4 +11,5 @@ SWEEP_ROUNDS=8 bash tools/gpu_run.sh gran || exit $?
 run c1_sched 300 python tools/c1_allreduce.py --ranks 2 --iters 200 --sched
 run c1_nosched 300 python tools/c1_allreduce.py --ranks 2 --iters 200
 run c1_oracle 300 python tools/c1_allreduce.py --ranks 2 --iters 200 --reduce oracle
+SMALLW_ELEMS="1024 16384" SMALLW_MODES="copy copyhost memcpy" bash tools/gpu_run.sh smallw || exit $?
 bash tools/gpu_run.sh smoke tests

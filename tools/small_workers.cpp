@@ -11,6 +11,10 @@
 //   ref      the reference's own compiled ccl_comp_reduce_regular
 //            (oracle/_ref/libref_ccl_comp.so, dlopen'ed lazily): the CPU loop
 //            the drop-in must not lose to
+//   copy     ccl_comp_copy of the buffer (classifies both pointers)
+//   copyhost ccl_comp_copy_host, the copy entries' call after
+//            integration/0006 (host to host, nothing looked up)
+//   memcpy   plain memcpy: the reference's ccl_comp_copy (comp.cpp:60-74)
 // Also prints the HIP pointer lookups the drop-in made per call.
 #include <dlfcn.h>
 
@@ -57,8 +61,12 @@ int main(int argc, char** argv) {
                 mi_ccl_comp_register_host_buffer(b.data(), n * sizeof(float));
             }
             if (mode == "sched") mi_ccl_comp_shim_sched(1);
+            const size_t nb = n * sizeof(float);
             auto call = [&] {
                 if (ref) ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0);
+                else if (mode == "copy") mi_ccl_comp_copy(a.data(), b.data(), nb, 0);
+                else if (mode == "copyhost") mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0);
+                else if (mode == "memcpy") memcpy(b.data(), a.data(), nb);
                 else mi_ccl_comp_reduce(a.data(), n, b.data(), nullptr, 9, 0);
             };
             for (long i = 0; i < std::min<long>(2000, iters); i++) call();
