@@ -139,3 +139,43 @@ def test_device_operands_under_a_stream_schedule():
         shim.mi_ccl_comp_shim_sched(prev)
     torch.cuda.synchronize()
     assert torch.equal(b.cpu().view(torch.int32), exp.view(torch.int32))
+
+
+def test_host_schedule_concurrent_workers_mixed_sizes():
+    """Eight workers under host schedules (as oneCCL's CPU-build entries call)
+    reduce host buckets from 4 KiB to 24 MiB at once: the small ones on their
+    own CPU with no lookup, the large ones split with the GPU; every result
+    is the oracle's."""
+    import threading
+    b_impl, f_impl = _impls()
+    sizes = [1024, 262144, (24 << 20) // 4 + 3]
+    errors = []
+
+    def worker(w):
+        shim = _lib.shim()
+        shim.mi_ccl_comp_shim_sched(1)
+        try:
+            for rep in range(2):
+                for n in sizes:
+                    a = rand_array(FP32, n, seed=1000 + 17 * w + n % 97 + rep, specials=False)
+                    b = rand_array(FP32, n, seed=2000 + 31 * w + n % 89 + rep, specials=False)
+                    exp = b.copy()
+                    oracle.comp_reduce(a, exp, FP32, 0, b_impl, f_impl)
+                    n0 = shim.mi_ccl_comp_pointer_lookups()
+                    rc = shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, FP32, 0)
+                    if rc != 0:
+                        errors.append((w, n, "rc", shim.mi_ccl_last_error()))
+                        continue
+                    if n * 4 <= (16 << 20) and shim.mi_ccl_comp_pointer_lookups() != n0:
+                        errors.append((w, n, "lookup"))
+                    if not np.array_equal(b.view(np.uint32), exp.view(np.uint32)):
+                        errors.append((w, n, "bits"))
+        finally:
+            shim.mi_ccl_comp_shim_sched(0)
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert errors == []
