@@ -11,7 +11,11 @@ and K fresh 1 GiB inputs, and times 20 in-place launches of the library's
 reduce (mi_reduce for K = 2, mi_reduce_multi otherwise) between HIP events.
 One JSON line per trial, then a summary line.
 
-  python tools/placement_probe.py [--inputs 2] [--trials 12] [--seed 1]
+  python tools/placement_probe.py [--inputs 2] [--trials 12] [--seed 1] [--offsets]
+--offsets (2 inputs): in each trial `in` is allocated 2 MiB larger and the
+same launch is timed with `in` shifted by 0, 4 KiB, 64 KiB and 1 MiB from its
+start, so the two operands' relative alignment changes while their pages do
+not.
 """
 from __future__ import annotations
 
@@ -31,6 +35,7 @@ def main() -> None:
     ap.add_argument("--trials", type=int, default=12)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--offsets", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -41,6 +46,8 @@ def main() -> None:
     k = a.inputs
     rng = random.Random(a.seed)
     meds = []
+    if a.offsets:
+        return offsets_mode(a, m, s, n, rng)
     for trial in range(a.trials):
         torch.cuda.empty_cache()
         pad_mib = 2 * rng.randrange(0, 1536)
@@ -74,8 +81,51 @@ def main() -> None:
     print(json.dumps({"summary": True, "inputs": k, "trials": a.trials, "min_ms": round(min(meds), 5),
                       "median_ms": round(statistics.median(meds), 5), "max_ms": round(max(meds), 5),
                       "spread": round(max(meds) / min(meds) - 1, 4),
-                      "frac_of_8TBps_best": round((k + 1) * (1 << 30) / min(meds) / 1e9 / 8000, 4),
-                      "frac_of_8TBps_worst": round((k + 1) * (1 << 30) / max(meds) / 1e9 / 8000, 4)}), flush=True)
+                      "frac_of_8TBps_best": round((k + 1) * (1 << 30) / (min(meds) / 1e3) / 1e12 / 8.0, 4),
+                      "frac_of_8TBps_worst": round((k + 1) * (1 << 30) / (max(meds) / 1e3) / 1e12 / 8.0, 4)}),
+          flush=True)
+
+
+def offsets_mode(a, m, s, n, rng):
+    import torch
+
+    from oneccl_amd import _lib
+    offs = [0, 4096, 65536, 1 << 20]
+    rows = []
+    for trial in range(a.trials):
+        torch.cuda.empty_cache()
+        pad_mib = 2 * rng.randrange(0, 1536)
+        pad = torch.empty(pad_mib << 18, dtype=torch.float32, device="cuda") if pad_mib else None
+        acc = torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+        inb = torch.empty(n + (2 << 20) // 4, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+        res = {}
+        for off in offs:
+            pin = inb.data_ptr() + off
+
+            def launch():
+                return m.mi_reduce(pin, acc.data_ptr(), n, 9, 0, 0, s.cuda_stream)
+
+            for _ in range(3):
+                _lib.check(launch())
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.launches):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                _lib.check(launch())
+                e1.record(s)
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ts.sort()
+            res[off] = round(ts[len(ts) // 2], 5)
+        rows.append(res)
+        print(json.dumps({"trial": trial, "pad_MiB": pad_mib, "median_ms_by_in_offset": res,
+                          "addr_GiB": [round(acc.data_ptr() / 2**30, 3), round(inb.data_ptr() / 2**30, 3)]}),
+              flush=True)
+        del acc, inb, pad
+    print(json.dumps({"summary": True, "mode": "offsets", "trials": a.trials,
+                      "median_ms_by_in_offset": {o: round(statistics.median(r[o] for r in rows), 5) for o in offs},
+                      "max_ms_by_in_offset": {o: max(r[o] for r in rows) for o in offs}}), flush=True)
 
 
 if __name__ == "__main__":
