@@ -1,0 +1,150 @@
+// pair_variants.hip — C2's placement mode against the order in which the
+// 2-input in-place reduce walks its tiles.
+//
+// tools/pair_probe.py found that the 1 GiB fp32 reduce runs ~7 % slower for
+// some pairs of buffers than for others, that the slow/fast outcome is a
+// property of the (acc, in) pair (fresh allocations fall in classes: same
+// class fast, different class slow), and that one buffer read or written
+// alone is never slower.  The kernel cannot see physical addresses, but it
+// decides which tiles are in flight together.  This tool allocates four
+// 1 GiB buffers, and for every ordered pair times the library's launch
+// (mi_reduce) and the same fold with other tile orders:
+//   map 0  tile = block (the library's order, this tool's own kernel)
+//   map 1  two halves interleaved: tile = (b % 2) * T/2 + b / 2
+//   map 2  8 regions interleaved (one per XCD under round-robin dispatch)
+//   map 3  64 regions interleaved
+//   map 4  tile = block, `in` loaded before `acc`
+// Each variant's output is checked against the library's on the first pair.
+//   pair_variants [rounds=3] [launches=10]        one JSON line per pair x variant
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../include/mi_reduce.h"
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(2);                                                                     \
+        }                                                                                \
+    } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MAP>
+__global__ __launch_bounds__(64) void fold2(f32x4* acc, const f32x4* in, uint64_t tiles) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    const uint64_t b = blockIdx.x;
+    uint64_t t;
+    if (MAP == 1) t = (b & 1) * (tiles / 2) + (b >> 1);
+    else if (MAP == 2) t = (b & 7) * (tiles / 8) + (b >> 3);
+    else if (MAP == 3) t = (b & 63) * (tiles / 64) + (b >> 6);
+    else t = b;
+    const uint64_t v = t * 64 + threadIdx.x;
+    f32x4 x, y;
+    if (MAP == 4) {
+        y = __builtin_nontemporal_load(in + v);
+        x = __builtin_nontemporal_load(acc + v);
+    } else {
+        x = __builtin_nontemporal_load(acc + v);
+        y = __builtin_nontemporal_load(in + v);
+    }
+    const f32x4 r = x + y;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(acc + t * 64), (short)0,
+                                                                  1024, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, r), rs,
+                                           threadIdx.x * 16u, 0, 18 /* sc1 nt, as the library */);
+}
+
+__global__ void fill(float* p, uint64_t n, uint32_t seed) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 13;
+        h *= 0x5bd1e995u;
+        p[i] = (float)(h & 0xFFFF) / 65536.0f - 0.5f;
+    }
+}
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 3;
+    const int launches = argc > 2 ? atoi(argv[2]) : 10;
+    const uint64_t bytes = 1ull << 30, n = bytes / 4, tiles = bytes / 1024;
+    float* buf[4];
+    for (auto& p : buf) CK(hipMalloc(&p, bytes));
+    float *chk_a, *chk_b;
+    CK(hipMalloc(&chk_a, bytes));
+    CK(hipMalloc(&chk_b, bytes));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    int dev = 0, ldsb = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&ldsb, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+    int waves = 0;
+    unsigned lib_lds = 0;
+    mi_get_residency(dev, 2, &waves, &lib_lds);
+    auto refill = [&](int i) { hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, s, buf[i], n, 0x9E37u + i); };
+    for (int i = 0; i < 4; i++) refill(i);
+    CK(hipStreamSynchronize(s));
+
+    auto run = [&](int v, float* acc, const float* in) -> hipError_t {
+        const dim3 g((unsigned)tiles), bl(64);
+        switch (v) {
+            case 0: hipLaunchKernelGGL(fold2<0>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 1: hipLaunchKernelGGL(fold2<1>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 2: hipLaunchKernelGGL(fold2<2>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 3: hipLaunchKernelGGL(fold2<3>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 4: hipLaunchKernelGGL(fold2<4>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            default: return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
+        }
+        return hipGetLastError();
+    };
+    const char* names[6] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
+                            "in loaded first", "library (mi_reduce)"};
+
+    // every variant's bits against the library's on one pair
+    for (int v = 0; v < 5; v++) {
+        CK(hipMemcpyAsync(chk_a, buf[0], bytes, hipMemcpyDeviceToDevice, s));
+        CK(hipMemcpyAsync(chk_b, buf[0], bytes, hipMemcpyDeviceToDevice, s));
+        CK(run(v, chk_a, buf[1]));
+        CK(run(5, chk_b, buf[1]));
+        CK(hipStreamSynchronize(s));
+        std::vector<uint32_t> ha(1 << 20), hb(1 << 20);
+        bool same = true;
+        for (uint64_t off = 0; off < n && same; off += (n / 8)) {
+            CK(hipMemcpy(ha.data(), chk_a + off, ha.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hb.data(), chk_b + off, hb.size() * 4, hipMemcpyDeviceToHost));
+            same = memcmp(ha.data(), hb.data(), ha.size() * 4) == 0;
+        }
+        printf("{\"check\": \"%s\", \"same_bits_as_library\": %s}\n", names[v], same ? "true" : "false");
+        if (!same) return 3;
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int r = 0; r < rounds; r++)
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) {
+                if (i == j) continue;
+                for (int v : {5, 0, 1, 2, 3, 4}) {
+                    for (int w = 0; w < 2; w++) CK(run(v, buf[i], buf[j]));
+                    CK(hipEventRecord(e0, s));
+                    for (int l = 0; l < launches; l++) CK(run(v, buf[i], buf[j]));
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    printf("{\"round\": %d, \"pair\": \"%d%d\", \"variant\": \"%s\", \"ms\": %.5f}\n", r, i, j, names[v],
+                           ms / launches);
+                    fflush(stdout);
+                }
+                refill(i);
+            }
+    return 0;
+}
