@@ -14,8 +14,12 @@
 //   map 2  8 regions interleaved (one per XCD under round-robin dispatch)
 //   map 3  64 regions interleaved
 //   map 4  tile = block, `in` loaded before `acc`
+//   map 5  walked backwards: tile = T - 1 - block
+//   map 6  two windows from both ends: even blocks from the start, odd from the end
 // Each variant's output is checked against the library's on the first pair.
-//   pair_variants [rounds=3] [launches=10]        one JSON line per pair x variant
+// `trials` times the buffers are freed and reallocated behind random pads, so
+// that pairs of both placement classes turn up.
+//   pair_variants [trials=4] [launches=10]        one JSON line per pair x variant
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -46,6 +50,8 @@ __global__ __launch_bounds__(64) void fold2(f32x4* acc, const f32x4* in, uint64_
     if (MAP == 1) t = (b & 1) * (tiles / 2) + (b >> 1);
     else if (MAP == 2) t = (b & 7) * (tiles / 8) + (b >> 3);
     else if (MAP == 3) t = (b & 63) * (tiles / 64) + (b >> 6);
+    else if (MAP == 5) t = tiles - 1 - b;
+    else if (MAP == 6) t = (b & 1) ? tiles - 1 - (b >> 1) : (b >> 1);
     else t = b;
     const uint64_t v = t * 64 + threadIdx.x;
     f32x4 x, y;
@@ -73,11 +79,13 @@ __global__ void fill(float* p, uint64_t n, uint32_t seed) {
 }
 
 int main(int argc, char** argv) {
-    const int rounds = argc > 1 ? atoi(argv[1]) : 3;
+    const int trials = argc > 1 ? atoi(argv[1]) : 4;
     const int launches = argc > 2 ? atoi(argv[2]) : 10;
     const uint64_t bytes = 1ull << 30, n = bytes / 4, tiles = bytes / 1024;
     float* buf[4];
     for (auto& p : buf) CK(hipMalloc(&p, bytes));
+    std::vector<void*> pads;
+    srand(7);
     float *chk_a, *chk_b;
     CK(hipMalloc(&chk_a, bytes));
     CK(hipMalloc(&chk_b, bytes));
@@ -101,15 +109,17 @@ int main(int argc, char** argv) {
             case 2: hipLaunchKernelGGL(fold2<2>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 3: hipLaunchKernelGGL(fold2<3>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 4: hipLaunchKernelGGL(fold2<4>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 6: hipLaunchKernelGGL(fold2<5>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 7: hipLaunchKernelGGL(fold2<6>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             default: return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
         }
         return hipGetLastError();
     };
-    const char* names[6] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
-                            "in loaded first", "library (mi_reduce)"};
+    const char* names[8] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
+                            "in loaded first", "library (mi_reduce)", "walked backwards", "two windows from both ends"};
 
     // every variant's bits against the library's on one pair
-    for (int v = 0; v < 5; v++) {
+    for (int v : {0, 1, 2, 3, 4, 6, 7}) {
         CK(hipMemcpyAsync(chk_a, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(hipMemcpyAsync(chk_b, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(run(v, chk_a, buf[1]));
@@ -128,11 +138,24 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int r = 0; r < rounds; r++)
+    for (int r = 0; r < trials; r++) {
+        if (r > 0) {  // new placement: free, pad at random, reallocate, refill
+            for (auto& p : buf) CK(hipFree(p));
+            for (void* p : pads) CK(hipFree(p));
+            pads.clear();
+            for (int i = 0; i < 4; i++) {
+                void* pad = nullptr;
+                CK(hipMalloc(&pad, (size_t)(1 + rand() % 512) << 21));
+                pads.push_back(pad);
+                CK(hipMalloc(&buf[i], bytes));
+                refill(i);
+            }
+            CK(hipStreamSynchronize(s));
+        }
         for (int i = 0; i < 4; i++)
             for (int j = 0; j < 4; j++) {
                 if (i == j) continue;
-                for (int v : {5, 0, 1, 2, 3, 4}) {
+                for (int v : {5, 0, 1, 4, 6, 7}) {
                     for (int w = 0; w < 2; w++) CK(run(v, buf[i], buf[j]));
                     CK(hipEventRecord(e0, s));
                     for (int l = 0; l < launches; l++) CK(run(v, buf[i], buf[j]));
@@ -146,5 +169,6 @@ int main(int argc, char** argv) {
                 }
                 refill(i);
             }
+    }
     return 0;
 }
