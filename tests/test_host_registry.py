@@ -266,3 +266,22 @@ def test_more_reader_threads_than_slots():
     t.join()
     assert res == [2]
     assert m.mi_host_undeclare(buf.ctypes.data) == 0
+
+
+def test_registry_stress_program(tmp_path):
+    """tests/cpp/registry_stress.cpp against the in-tree library (no sanitizer,
+    ~1 s): readers, writers and short-lived reader threads at once.  The same
+    program under TSan and ASan builds of the host code is
+    tools/sanitize_registry.sh (profiles/round4_sanitizers/)."""
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "registry_stress"
+    r = subprocess.run(["g++", "-O1", "-std=c++17", f"-I{root / 'include'}", "-o", str(exe),
+                        str(root / "tests" / "cpp" / "registry_stress.cpp"), f"-L{root / 'oneccl_amd' / 'lib'}",
+                        "-lmi_reduce", f"-Wl,-rpath,{root / 'oneccl_amd' / 'lib'}", "-pthread"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run([str(exe), "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
+    assert "failures 0" in r.stdout
