@@ -8,7 +8,13 @@ allocated; each is read alone and written alone by the memory-only probes
 (libmi_ceiling.so, best flavour), and every ordered pair is reduced in place
 (acc, in) with mi_reduce.  One JSON line per trial.
 
-  python tools/pair_probe.py [--trials 4] [--buffers 4]
+--streams: per ordered pair also the reduce's traffic without its arithmetic,
+so that the slow mode can be pinned on one interaction: both buffers read at
+once (`read2`), `in` copied onto `acc` by the library's copy kernel (`copy`:
+read one, write the other), and `acc` rewritten from itself (`self`: the
+in-place read-modify-write of one buffer, mi_copy with src == dst).
+
+  python tools/pair_probe.py [--trials 4] [--buffers 4] [--streams]
 """
 from __future__ import annotations
 
@@ -30,6 +36,7 @@ def main() -> None:
     ap.add_argument("--buffers", type=int, default=4)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--streams", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -74,9 +81,19 @@ def main() -> None:
         for i, j in itertools.permutations(range(a.buffers), 2):
             acc, inp = bufs[i], bufs[j]
             pairs[f"{i}{j}"] = timed(lambda: m.mi_reduce(inp.data_ptr(), acc.data_ptr(), n, 9, 0, 0, sh))
-        print(json.dumps({"trial": trial, "pad_MiB": pad_mib, "read_1stream_ms": read1, "write_ms": write1,
-                          "reduce_ms_acc_in": pairs,
-                          "addr_GiB": [round(b.data_ptr() / 2**30, 3) for b in bufs]}), flush=True)
+        row = {"trial": trial, "pad_MiB": pad_mib, "read_1stream_ms": read1, "write_ms": write1,
+               "reduce_ms_acc_in": pairs, "addr_GiB": [round(b.data_ptr() / 2**30, 3) for b in bufs]}
+        if a.streams:
+            read2, copy, self_ = {}, {}, {}
+            for i, j in itertools.permutations(range(a.buffers), 2):
+                acc, inp = bufs[i], bufs[j]
+                arr = _lib.void_ptr_array([acc.data_ptr(), inp.data_ptr()])
+                read2[f"{i}{j}"] = timed(lambda: L.mic_read_streams(arr, 2, nb, 64, 0, 0, sink.data_ptr(), sh))
+                copy[f"{i}{j}"] = timed(lambda: m.mi_copy(inp.data_ptr(), acc.data_ptr(), nb, 1, sh))
+            for i, b in enumerate(bufs):
+                self_[i] = timed(lambda: m.mi_copy(b.data_ptr(), b.data_ptr(), nb, 1, sh))
+            row.update({"read2_ms_acc_in": read2, "copy_ms_in_to_acc": copy, "self_copy_ms": self_})
+        print(json.dumps(row), flush=True)
         del bufs, pad
 
 
