@@ -362,6 +362,12 @@ int mi_get_launch_config(int* block, int* unroll, int* max_blocks);
  * (no cap then).  DESIGN.md §5; tools/occupancy_sweep.hip measured the
  * caps.                                                                    */
 int mi_get_residency(int device, int k, int* waves_per_cu, unsigned* lds_bytes);
+/* Override that plan for k-input launches (tuning knob, k as above):
+ * waves_per_cu 1..32 (the reservation is 128 / waves_per_cu whole LDS
+ * granules, so the residency achieved is one of 32, 25, 21, 18, 16, 14, 12,
+ * 11, 10, 9, 8, ...), 0 = back to the plan.
+ * tools/residency_ab.py A/Bs the plan against other residencies with it.  */
+int mi_set_residency(int k, int waves_per_cu);
 /* Override the grid cap (tuning knob; env MI_REDUCE_MAX_BLOCKS).  Under a
  * cap the reduce, copy and conversion kernels stride over the buffer.     */
 int mi_set_max_blocks(int max_blocks);

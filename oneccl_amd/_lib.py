@@ -81,6 +81,7 @@ MI_API = [
     ("mi_get_launch_config", c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     ("mi_get_residency", c_int, [c_int, c_int, POINTER(c_int), POINTER(c_uint)]),
     ("mi_set_max_blocks", c_int, [c_int]),
+    ("mi_set_residency", c_int, [c_int, c_int]),
     ("mi_set_host_mode", c_int, [c_int]),
     ("mi_set_sync_mode", c_int, [c_int]),
     ("mi_set_unaligned_vectors", c_int, [c_int]),

@@ -184,6 +184,17 @@ constexpr int kLeanWavesPerCU = 21;
 constexpr int kFanBlock = 64;
 // (achieved residencies of round 3's caps 16 / 12 / 10 / 8 / 6, see above)
 int fan_waves_per_cu(int k) { return k <= 4 ? 16 : k <= 6 ? 11 : k <= 8 ? 9 : k <= 12 ? 8 : 5; }
+constexpr int kConvWavesPerCU = 21;  // the array conversions (achieved residency of round 3's cap of 24)
+
+// mi_set_residency overrides (tuning, per k as mi_get_residency: 0 the
+// conversions, 2 the 2-input kernel, 1 and 3..16 the fan-in); 0 = the plan
+std::atomic<int> g_residency_override[MI_MAX_INPUTS + 1];
+
+int planned_waves(int k) {
+    const int o = g_residency_override[k].load(std::memory_order_relaxed);
+    if (o > 0) return o;
+    return k == 2 ? kLeanWavesPerCU : k == 0 ? kConvWavesPerCU : fan_waves_per_cu(k);
+}
 
 // LDS bytes per CU of each device (read once per device; 0 = unknown: no
 // cap).  Lock-free: every launch reads it, from any number of threads.
@@ -569,7 +580,7 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         const uint64_t tile = (uint64_t)kB2 * kU2;
         uint64_t blocks = std::max<uint64_t>((nvec + tile - 1) / tile, 1);
         if (blocks > 0x7FFFFFFFull) return fail(MI_E_UNSUPPORTED, "bucket too large for one launch");
-        e = kern.lean(dim3((unsigned)blocks), stream, r, wave_cap_lds(stream, kLeanWavesPerCU));
+        e = kern.lean(dim3((unsigned)blocks), stream, r, wave_cap_lds(stream, planned_waves(2)));
     } else {
         KArgs a;
         memset(&a, 0, sizeof(a));
@@ -587,7 +598,7 @@ int launch_reduce(const void* const* inputs, int k, void* out, size_t count, int
         }
         // fan tiles are 64 vectors: one launch covers 2^37 vectors (2 TiB)
         if (vec && cap == 0 && nvec / kFanBlock < 0x7FFFFFFFull) {
-            e = kern.fan(stream, a, wave_cap_lds(stream, fan_waves_per_cu(k)));
+            e = kern.fan(stream, a, wave_cap_lds(stream, planned_waves(k)));
         } else {
             uint64_t blocks;
             if (vec) {
@@ -674,7 +685,7 @@ int launch_reduce_batch(const mi_reduce_desc_t* d, int n, int dt, int op, unsign
     auto flush = [&]() -> int {
         if (!a.n) return 0;
         a.block0[a.n] = (uint32_t)blocks;
-        const hipError_t e = kern.batch(dim3((unsigned)blocks), stream, a, wave_cap_lds(stream, kLeanWavesPerCU));
+        const hipError_t e = kern.batch(dim3((unsigned)blocks), stream, a, wave_cap_lds(stream, planned_waves(2)));
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
         memset(&a, 0, sizeof(a));
         blocks = 0;
@@ -1475,7 +1486,6 @@ typedef hipError_t (*ConvFn)(dim3, hipStream_t, const CArgs&, unsigned lds);
 // bf16 0.253 -> 0.243 ms, bf16 -> fp32 0.262 -> 0.239 ms against round 2's
 // 256-lane blocks (tools/occupancy_sweep.hip copyconv, profiles/round3_occupancy/).
 constexpr int kConvBlock = 64;
-constexpr int kConvWavesPerCU = 21;  // achieved residency of round 3's cap of 24 (see kLeanWavesPerCU)
 
 template <typename ST, typename DT, unsigned V>
 hipError_t conv_one(dim3 grid, hipStream_t s, const CArgs& a, unsigned lds) {
@@ -1523,7 +1533,7 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     const int cap = max_blocks();  // a grid cap (mi_set_max_blocks) makes the kernel stride
     if (cap > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cap);
     blocks = std::max<uint64_t>(blocks, 1);
-    hipError_t e = fn(dim3((unsigned)blocks), s, a, wave_cap_lds(s, kConvWavesPerCU));
+    hipError_t e = fn(dim3((unsigned)blocks), s, a, wave_cap_lds(s, planned_waves(0)));
     if (e != hipSuccess) return hip_fail(e, "convert kernel launch");
     return 0;
 }
@@ -2198,9 +2208,16 @@ int mi_get_launch_config(int* block, int* unroll, int* max_blocks_out) {
 int mi_get_residency(int device, int k, int* waves_per_cu, unsigned* lds_bytes) {
     if (k < 0 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "k must be 0..16");
     if (device < 0 && hipGetDevice(&device) != hipSuccess) device = -1;
-    const int w = k == 2 ? kLeanWavesPerCU : k == 0 ? kConvWavesPerCU : fan_waves_per_cu(k);
+    const int w = planned_waves(k);
     if (waves_per_cu) *waves_per_cu = w;
     if (lds_bytes) *lds_bytes = wave_cap_enabled() ? wave_cap_bytes(lds_per_cu(device), w) : 0;
+    return 0;
+}
+
+int mi_set_residency(int k, int waves_per_cu) {
+    if (k < 0 || k > MI_MAX_INPUTS) return fail(MI_E_INVALID, "k must be 0..16");
+    if (waves_per_cu < 0 || waves_per_cu > 32) return fail(MI_E_INVALID, "waves_per_cu must be 0..32");
+    g_residency_override[k].store(waves_per_cu, std::memory_order_relaxed);
     return 0;
 }
 

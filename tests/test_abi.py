@@ -178,3 +178,22 @@ def test_residency_plan():
             assert lds.value == 0
     assert m.mi_get_residency(-1, 17, ctypes.byref(w), ctypes.byref(lds)) == -1
     assert m.mi_get_residency(-1, -1, None, None) == -1
+
+
+def test_residency_override():
+    """mi_set_residency (tuning knob): replaces the plan for one k, is
+    reported by mi_get_residency, and 0 restores the plan."""
+    m = _lib.mi()
+    w = ctypes.c_int()
+    try:
+        assert m.mi_set_residency(2, 18) == 0
+        assert m.mi_get_residency(-1, 2, ctypes.byref(w), None) == 0 and w.value == 18
+        assert m.mi_get_residency(-1, 8, ctypes.byref(w), None) == 0 and w.value == 9  # other k untouched
+        assert m.mi_set_residency(8, 32) == 0
+        assert m.mi_get_residency(-1, 8, ctypes.byref(w), None) == 0 and w.value == 32
+    finally:
+        assert m.mi_set_residency(2, 0) == 0 and m.mi_set_residency(8, 0) == 0
+    assert m.mi_get_residency(-1, 2, ctypes.byref(w), None) == 0 and w.value == 21
+    assert m.mi_get_residency(-1, 8, ctypes.byref(w), None) == 0 and w.value == 9
+    assert m.mi_set_residency(17, 8) == -1 and m.mi_set_residency(-1, 8) == -1
+    assert m.mi_set_residency(2, 33) == -1 and m.mi_set_residency(2, -1) == -1

@@ -16,10 +16,15 @@
 //   map 4  tile = block, `in` loaded before `acc`
 //   map 5  walked backwards: tile = T - 1 - block
 //   map 6  two windows from both ends: even blocks from the start, odd from the end
+// and, in library order, other residencies (the slow mode has fewer reads in
+// flight at the L2, placement_pmc/): 16 and 25 resident waves per CU, no cap,
+// and two tiles per wave at the library's cap.
 // Each variant's output is checked against the library's on the first pair.
 // `trials` times the buffers are freed and reallocated behind random pads, so
 // that pairs of both placement classes turn up.
 //   pair_variants [trials=4] [launches=10]        one JSON line per pair x variant
+//   PAIR_RESIDENCY=1 pair_variants ...           the residency variants instead of the orders
+//   PAIR_WAVES=12,16,21 pair_variants ...        the library's order at these wave caps
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -69,6 +74,21 @@ __global__ __launch_bounds__(64) void fold2(f32x4* acc, const f32x4* in, uint64_
                                            threadIdx.x * 16u, 0, 18 /* sc1 nt, as the library */);
 }
 
+// two consecutive tiles per wave: four loads in flight per lane
+__global__ __launch_bounds__(64) void fold2x2(f32x4* acc, const f32x4* in, uint64_t tiles) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    const uint64_t t = (uint64_t)blockIdx.x * 2;
+    const uint64_t v = t * 64 + threadIdx.x;
+    const f32x4 x0 = __builtin_nontemporal_load(acc + v), x1 = __builtin_nontemporal_load(acc + v + 64);
+    const f32x4 y0 = __builtin_nontemporal_load(in + v), y1 = __builtin_nontemporal_load(in + v + 64);
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(acc + t * 64), (short)0,
+                                                                  2048, 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x0 + y0), rs, threadIdx.x * 16u, 0, 18);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x1 + y1), rs, 1024u + threadIdx.x * 16u, 0, 18);
+}
+
 __global__ void fill(float* p, uint64_t n, uint32_t seed) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t h = (uint32_t)i * 2654435761u ^ seed;
@@ -101,9 +121,24 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 4; i++) refill(i);
     CK(hipStreamSynchronize(s));
 
+    const unsigned gran = (unsigned)ldsb / 128u;
+    auto lds_for = [&](int w) { return (128u / (unsigned)w) * gran; };
     auto run = [&](int v, float* acc, const float* in) -> hipError_t {
         const dim3 g((unsigned)tiles), bl(64);
         switch (v) {
+            case 8: hipLaunchKernelGGL(fold2<0>, g, bl, lds_for(16), s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 9: hipLaunchKernelGGL(fold2<0>, g, bl, lds_for(25), s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            case 10: hipLaunchKernelGGL(fold2<0>, g, bl, 0, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
+            default:
+                if (v >= 100) {  // tile = block at a cap of v - 100 waves per CU
+                    hipLaunchKernelGGL(fold2<0>, g, bl, lds_for(v - 100), s, (f32x4*)acc, (const f32x4*)in, tiles);
+                    break;
+                }
+                return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
+            case 11:
+                hipLaunchKernelGGL(fold2x2, dim3((unsigned)(tiles / 2)), bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in,
+                                   tiles);
+                break;
             case 0: hipLaunchKernelGGL(fold2<0>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 1: hipLaunchKernelGGL(fold2<1>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 2: hipLaunchKernelGGL(fold2<2>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
@@ -111,15 +146,25 @@ int main(int argc, char** argv) {
             case 4: hipLaunchKernelGGL(fold2<4>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 6: hipLaunchKernelGGL(fold2<5>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
             case 7: hipLaunchKernelGGL(fold2<6>, g, bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in, tiles); break;
-            default: return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
+            case 5: return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
         }
         return hipGetLastError();
     };
-    const char* names[8] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
-                            "in loaded first", "library (mi_reduce)", "walked backwards", "two windows from both ends"};
+    const char* names[12] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
+                             "in loaded first", "library (mi_reduce)", "walked backwards", "two windows from both ends",
+                             "16 waves/CU", "25 waves/CU", "no wave cap", "two tiles per wave"};
+    const bool resid = getenv("PAIR_RESIDENCY") != nullptr;  // time the residency variants instead of the orders
+    std::vector<int> caps;  // PAIR_WAVES=12,16,21: the library's order at these caps instead
+    if (const char* w = getenv("PAIR_WAVES"))
+        for (const char* q = w; *q;) {
+            caps.push_back(100 + atoi(q));
+            while (*q && *q != ',') q++;
+            if (*q) q++;
+        }
+    auto name_of = [&](int v) { return v >= 100 ? std::to_string(v - 100) + " waves/CU" : std::string(names[v]); };
 
     // every variant's bits against the library's on one pair
-    for (int v : {0, 1, 2, 3, 4, 6, 7}) {
+    for (int v : {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11}) {
         CK(hipMemcpyAsync(chk_a, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(hipMemcpyAsync(chk_b, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(run(v, chk_a, buf[1]));
@@ -155,7 +200,12 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 4; i++)
             for (int j = 0; j < 4; j++) {
                 if (i == j) continue;
-                for (int v : {5, 0, 1, 4, 6, 7}) {
+                std::vector<int> vs = resid ? std::vector<int>{5, 0, 8, 9, 10, 11} : std::vector<int>{5, 0, 1, 4, 6, 7};
+                if (!caps.empty()) {
+                    vs = {5};
+                    vs.insert(vs.end(), caps.begin(), caps.end());
+                }
+                for (int v : vs) {
                     for (int w = 0; w < 2; w++) CK(run(v, buf[i], buf[j]));
                     CK(hipEventRecord(e0, s));
                     for (int l = 0; l < launches; l++) CK(run(v, buf[i], buf[j]));
@@ -163,7 +213,7 @@ int main(int argc, char** argv) {
                     CK(hipEventSynchronize(e1));
                     float ms = 0;
                     CK(hipEventElapsedTime(&ms, e0, e1));
-                    printf("{\"round\": %d, \"pair\": \"%d%d\", \"variant\": \"%s\", \"ms\": %.5f}\n", r, i, j, names[v],
+                    printf("{\"round\": %d, \"pair\": \"%d%d\", \"variant\": \"%s\", \"ms\": %.5f}\n", r, i, j, name_of(v).c_str(),
                            ms / launches);
                     fflush(stdout);
                 }
