@@ -424,10 +424,23 @@ def config_legs(m, stream, launches=10):
     from oneccl_amd import _lib
     legs = {}
     sh = stream.cuda_stream
-    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod"):
-        desc, dt, es, op, k, bucket, flags = CONFIGS[name]
+    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", "c2-one-allocation"):
+        one_alloc = name == "c2-one-allocation"
+        desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if one_alloc else name]
         n = bucket // es
-        ins = [torch.empty(n, dtype=torch_dtype(dt), device="cuda") for _ in range(k)]
+        if one_alloc:
+            # the headline's kernel and bucket with both operands carved from one
+            # allocation: separate 1 GiB allocations land in HBM placement classes
+            # and a pair across classes reads ~7 % slower; slices of one
+            # allocation were in the fast mode in 96 of 96 pairs
+            # (tools/pair_probe.py --slab)
+            desc = ("the headline (2-input fp32 sum, 1 GiB bucket) with acc and in as the two halves of one 2 GiB "
+                    "allocation, not two allocations")
+            slab = torch.empty(k * n, dtype=torch_dtype(dt), device="cuda")
+            ins = [slab[j * n:(j + 1) * n] for j in range(k)]
+            del slab
+        else:
+            ins = [torch.empty(n, dtype=torch_dtype(dt), device="cuda") for _ in range(k)]
         for j, t in enumerate(ins):
             fill(t, 0xC0 + 131 * j)
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])

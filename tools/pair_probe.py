@@ -14,7 +14,10 @@ once (`read2`), `in` copied onto `acc` by the library's copy kernel (`copy`:
 read one, write the other), and `acc` rewritten from itself (`self`: the
 in-place read-modify-write of one buffer, mi_copy with src == dst).
 
-  python tools/pair_probe.py [--trials 4] [--buffers 4] [--streams]
+--slab: the buffers are consecutive 1 GiB slices of one allocation, not
+allocations of their own.
+
+  python tools/pair_probe.py [--trials 4] [--buffers 4] [--streams] [--slab]
 """
 from __future__ import annotations
 
@@ -37,6 +40,7 @@ def main() -> None:
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--streams", action="store_true")
+    ap.add_argument("--slab", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -70,7 +74,11 @@ def main() -> None:
         torch.cuda.empty_cache()
         pad_mib = 2 * rng.randrange(0, 1536)
         pad = torch.empty(pad_mib << 18, dtype=torch.float32, device="cuda") if pad_mib else None
-        bufs = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1) for _ in range(a.buffers)]
+        if a.slab:
+            slab = torch.empty(a.buffers * n, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+            bufs = [slab[i * n:(i + 1) * n] for i in range(a.buffers)]
+        else:
+            bufs = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1) for _ in range(a.buffers)]
         read1, write1 = {}, {}
         for i, b in enumerate(bufs):
             arr = _lib.void_ptr_array([b.data_ptr()])
@@ -81,7 +89,7 @@ def main() -> None:
         for i, j in itertools.permutations(range(a.buffers), 2):
             acc, inp = bufs[i], bufs[j]
             pairs[f"{i}{j}"] = timed(lambda: m.mi_reduce(inp.data_ptr(), acc.data_ptr(), n, 9, 0, 0, sh))
-        row = {"trial": trial, "pad_MiB": pad_mib, "read_1stream_ms": read1, "write_ms": write1,
+        row = {"trial": trial, "slab": a.slab, "pad_MiB": pad_mib, "read_1stream_ms": read1, "write_ms": write1,
                "reduce_ms_acc_in": pairs, "addr_GiB": [round(b.data_ptr() / 2**30, 3) for b in bufs]}
         if a.streams:
             read2, copy, self_ = {}, {}, {}
@@ -95,6 +103,8 @@ def main() -> None:
             row.update({"read2_ms_acc_in": read2, "copy_ms_in_to_acc": copy, "self_copy_ms": self_})
         print(json.dumps(row), flush=True)
         del bufs, pad
+        if a.slab:
+            del slab
 
 
 if __name__ == "__main__":

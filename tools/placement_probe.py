@@ -11,7 +11,11 @@ and K fresh 1 GiB inputs, and times 20 in-place launches of the library's
 reduce (mi_reduce for K = 2, mi_reduce_multi otherwise) between HIP events.
 One JSON line per trial, then a summary line.
 
-  python tools/placement_probe.py [--inputs 2] [--trials 12] [--seed 1] [--offsets]
+  python tools/placement_probe.py [--inputs 2] [--trials 12] [--seed 1] [--offsets] [--layout L]
+--layout: `separate` (default) one allocation per input; `one` all K inputs
+consecutive slices of one allocation; `nreduce` the accumulator alone and the
+other K - 1 inputs in one allocation, as oneCCL's nreduce lays out the peers'
+chunks in its tmp buffer (allreduce.cpp:333-394).
 --offsets (2 inputs): in each trial `in` is allocated 2 MiB larger and the
 same launch is timed with `in` shifted by 0, 4 KiB, 64 KiB and 1 MiB from its
 start, so the two operands' relative alignment changes while their pages do
@@ -36,6 +40,7 @@ def main() -> None:
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--offsets", action="store_true")
+    ap.add_argument("--layout", choices=("separate", "one", "nreduce"), default="separate")
     a = ap.parse_args()
     import torch
 
@@ -52,7 +57,14 @@ def main() -> None:
         torch.cuda.empty_cache()
         pad_mib = 2 * rng.randrange(0, 1536)
         pad = torch.empty(pad_mib << 18, dtype=torch.float32, device="cuda") if pad_mib else None
-        ins = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1) for _ in range(k)]
+        if a.layout == "separate":
+            ins = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1) for _ in range(k)]
+        else:
+            first = 0 if a.layout == "one" else 1
+            ins = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1)] if first else []
+            slab = torch.empty((k - first) * n, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+            ins += [slab[j * n:(j + 1) * n] for j in range(k - first)]
+            del slab
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
 
         def launch():
@@ -74,11 +86,11 @@ def main() -> None:
         ts.sort()
         med = ts[len(ts) // 2]
         meds.append(med)
-        print(json.dumps({"trial": trial, "inputs": k, "pad_MiB": pad_mib, "median_ms": round(med, 5),
+        print(json.dumps({"trial": trial, "inputs": k, "layout": a.layout, "pad_MiB": pad_mib, "median_ms": round(med, 5),
                           "best_ms": round(ts[0], 5), "TBps_median": round((k + 1) * (1 << 30) / med / 1e9, 3),
                           "addr_GiB": [round(t.data_ptr() / 2**30, 3) for t in ins]}), flush=True)
         del ins, arr, pad
-    print(json.dumps({"summary": True, "inputs": k, "trials": a.trials, "min_ms": round(min(meds), 5),
+    print(json.dumps({"summary": True, "inputs": k, "layout": a.layout, "trials": a.trials, "min_ms": round(min(meds), 5),
                       "median_ms": round(statistics.median(meds), 5), "max_ms": round(max(meds), 5),
                       "spread": round(max(meds) / min(meds) - 1, 4),
                       "frac_of_8TBps_best": round((k + 1) * (1 << 30) / (min(meds) / 1e3) / 1e12 / 8.0, 4),
