@@ -68,6 +68,9 @@ def parse():
     p.add_argument("--no-host-leg", action="store_true", help="skip the host-resident (PCIe) measurement")
     p.add_argument("--no-config-legs", action="store_true",
                    help="skip the other BASELINE configs' legs (timed launches + full parity) of a c2 run")
+    p.add_argument("--layout", default="one", choices=["one", "separate"],
+                   help="one: a config's k inputs are consecutive slices of one allocation (default); separate: "
+                        "one allocation per input (DESIGN.md §6, placement modes)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
                         "one GPU when rehearsing the N>1 path)")
@@ -83,6 +86,21 @@ def fill(t, seed):
         t.uniform_(-1.0, 1.0, generator=g)
     else:
         t.random_(-1000, 1000, generator=g)
+
+
+def alloc_inputs(k, n, tdt, layout):
+    """The k input buffers of n elements.  layout "one": consecutive slices of
+    one allocation; "separate": an allocation each.  Separate allocations land
+    in HBM placement classes, and two read streams from buffers of different
+    classes run ~7 % slower (tools/pair_probe.py); slices of one
+    allocation do not split that way: the same median launch time as separate
+    allocations, 0.5-0.7 % spread instead of 7-10 %
+    (profiles/round4_run6/placement_probe_*.jsonl)."""
+    import torch
+    if layout == "one":
+        slab = torch.empty(k * n, dtype=tdt, device="cuda")
+        return [slab[j * n:(j + 1) * n] for j in range(k)]
+    return [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
 
 
 def torch_dtype(dt):
@@ -411,7 +429,7 @@ def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, w
             "scaling": "strong", "note": "one bucket split by element range over the ranks, no collective"}
 
 
-def config_legs(m, stream, launches=10):
+def config_legs(m, stream, layout, launches=10):
     """The other BASELINE.json configs, each at its full size on this GPU, in
     the same run as the headline: mean launch time of `launches` back-to-back
     launches under one event pair, and the whole result checked bit for bit
@@ -424,23 +442,16 @@ def config_legs(m, stream, launches=10):
     from oneccl_amd import _lib
     legs = {}
     sh = stream.cuda_stream
-    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", "c2-one-allocation"):
-        one_alloc = name == "c2-one-allocation"
-        desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if one_alloc else name]
+    other = "separate" if layout == "one" else "one"
+    c2_other = f"c2-layout-{other}"
+    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", c2_other):
+        desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if name == c2_other else name]
         n = bucket // es
-        if one_alloc:
-            # the headline's kernel and bucket with both operands carved from one
-            # allocation: separate 1 GiB allocations land in HBM placement classes
-            # and a pair across classes reads ~7 % slower; slices of one
-            # allocation were in the fast mode in 96 of 96 pairs
-            # (tools/pair_probe.py --slab)
-            desc = ("the headline (2-input fp32 sum, 1 GiB bucket) with acc and in as the two halves of one 2 GiB "
-                    "allocation, not two allocations")
-            slab = torch.empty(k * n, dtype=torch_dtype(dt), device="cuda")
-            ins = [slab[j * n:(j + 1) * n] for j in range(k)]
-            del slab
-        else:
-            ins = [torch.empty(n, dtype=torch_dtype(dt), device="cuda") for _ in range(k)]
+        if name == c2_other:
+            # the headline's kernel and bucket in the other buffer layout
+            desc = (f"the headline (2-input fp32 sum, 1 GiB bucket) with acc and in "
+                    + ("in two allocations" if other == "separate" else "as the two halves of one allocation"))
+        ins = alloc_inputs(k, n, torch_dtype(dt), other if name == c2_other else layout)
         for j, t in enumerate(ins):
             fill(t, 0xC0 + 131 * j)
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
@@ -661,7 +672,7 @@ def main():
         tmp = torch.empty((k - 1) * n, dtype=tdt, device="cuda")
         ins = [torch.empty(n, dtype=tdt, device="cuda")] + [tmp[j * n:(j + 1) * n] for j in range(k - 1)]
     else:
-        ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+        ins = alloc_inputs(k, n, tdt, args.layout)
     for j, t in enumerate(ins):
         fill(t, 0xC0FFEE + 7919 * rank + j)
     stream = torch.cuda.current_stream()
@@ -741,7 +752,7 @@ def main():
 
     legs = None
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_config_legs:
-        legs = config_legs(m, stream)
+        legs = config_legs(m, stream, args.layout)
 
     # BASELINE configs[3] as written at N > 1: one 1 GiB bucket split over the
     # GPUs, beside the weak-scaling `value` (each GPU its own 1 GiB bucket):
@@ -776,6 +787,10 @@ def main():
             "dtype": DTYPE_LABEL.get(dt, str(dt)),
             "data": "synthetic (uniform [-1,1) generated on device)",
             "config": {"workload": desc, "bucket_bytes_per_gpu": units_per_rank, "inputs": k,
+                       "layout": ("reduce_buf apart, the k - 1 peer chunks in one tmp allocation"
+                                  if args.config == "c4-tmpbuf" else
+                                  "the k inputs as consecutive slices of one allocation" if args.layout == "one"
+                                  else "one allocation per input"),
                        "op": ["sum", "prod", "min", "max"][op], "dtype_id": dt, "flags": flags,
                        "parallelism": f"element-range shard x{world}, no collective",
                        "entry": "mi_reduce (include/mi_reduce.h) via ctypes, async on the torch stream"},
