@@ -392,7 +392,7 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
 
 
 def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None,
-                 n_devices=None):
+                 n_devices=None, layout="one"):
     """One bucket of n_total elements split by element range over the ranks
     (mi_shard_range, 256-element aligned; BASELINE configs[3] as written):
     this rank reduces its shard of all k inputs.  `ins` (optional) holds
@@ -402,7 +402,7 @@ def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, w
     n, _, total_bytes = plan(n_total, es, rank, world, "strong")
     tdt = torch_dtype(dt)
     if ins is None:
-        ins = [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+        ins = alloc_inputs(k, n, tdt, layout)
         for j, t in enumerate(ins):
             fill(t, 0xA0 + j + 7919 * rank)
     from oneccl_amd import _lib
@@ -764,7 +764,7 @@ def main():
         del ins
         torch.cuda.empty_cache()
         strong["c4_fanin8"] = strong_split(m, 9, 4, 0, 8, 0, GiB // 4, rank, world, stream, args.steps,
-                                           args.warmup, coll_dev, n_devices=n_devices)
+                                           args.warmup, coll_dev, n_devices=n_devices, layout=args.layout)
         torch.cuda.empty_cache()
 
     traffic = pmc_traffic(args.config, traffic_per_launch)
