@@ -414,8 +414,11 @@ ReaderSlot* reader_slot() {
         t_reader.idx = -1;
         for (int i = 0; i < kReaderSlots; i++) {
             bool f = false;
+            // seq_cst, as the writer's load of `used`: a writer that published
+            // before this thread's first read either sees the slot taken or
+            // is seen by the read (it then loads the new snapshot)
             if (!g_readers[i].used.load(std::memory_order_relaxed) &&
-                g_readers[i].used.compare_exchange_strong(f, true, std::memory_order_acq_rel)) {
+                g_readers[i].used.compare_exchange_strong(f, true, std::memory_order_seq_cst)) {
                 t_reader.idx = i;
                 break;
             }
