@@ -68,9 +68,10 @@ def parse():
     p.add_argument("--no-host-leg", action="store_true", help="skip the host-resident (PCIe) measurement")
     p.add_argument("--no-config-legs", action="store_true",
                    help="skip the other BASELINE configs' legs (timed launches + full parity) of a c2 run")
-    p.add_argument("--layout", default="one", choices=["one", "separate"],
-                   help="one: a config's k inputs are consecutive slices of one allocation (default); separate: "
-                        "one allocation per input (DESIGN.md §6, placement modes)")
+    p.add_argument("--layout", default="padded", choices=LAYOUTS,
+                   help="padded (default): a config's inputs in one allocation, a 2-input config's operands "
+                        f"{PAIR_GAP >> 20} MiB apart beyond the bucket; one: consecutive slices of one allocation; "
+                        "separate: one allocation per input (DESIGN.md §6, placement modes)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
                         "one GPU when rehearsing the N>1 path)")
@@ -88,19 +89,32 @@ def fill(t, seed):
         t.random_(-1000, 1000, generator=g)
 
 
+LAYOUTS = ("padded", "one", "separate")
+PAIR_GAP = 896 << 20  # bytes between the two operands of a padded layout
+LAYOUT_NOTE = {
+    "padded": f"the inputs in one allocation; a 2-input config's operands {PAIR_GAP >> 20} MiB apart beyond the bucket",
+    "one": "the inputs as consecutive slices of one allocation",
+    "separate": "one allocation per input",
+}
+
+
 def alloc_inputs(k, n, tdt, layout):
-    """The k input buffers of n elements.  layout "one": consecutive slices of
-    one allocation; "separate": an allocation each.  Separate allocations land
-    in HBM placement classes, and two read streams from buffers of different
-    classes run ~7 % slower (tools/pair_probe.py); slices of one
-    allocation do not split that way: the same median launch time as separate
-    allocations, 0.5-0.7 % spread instead of 7-10 %
-    (profiles/round4_run6/placement_probe_*.jsonl)."""
+    """The k input buffers of n elements.  Where the operands sit relative to
+    each other decides the 2-input reduce's rate by up to 7 % (DESIGN.md §6,
+    "Where the run-to-run spread comes from"): separate allocations draw a
+    placement per run (fast, medium or slow: 0.471-0.511 ms for C2); slices of
+    one allocation run at one rate whose level follows their offset (C2: 0.480
+    ms at 1 GiB, 0.473-0.475 at 1 GiB + 896 MiB on two boxes,
+    profiles/round4_run7/).  "padded" puts a 2-input config's operands
+    PAIR_GAP apart beyond the bucket and is contiguous for a fan-in (whose rate
+    no gap steadied); "one" is contiguous; "separate" is an allocation each."""
     import torch
-    if layout == "one":
-        slab = torch.empty(k * n, dtype=tdt, device="cuda")
-        return [slab[j * n:(j + 1) * n] for j in range(k)]
-    return [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+    if layout == "separate":
+        return [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+    es = torch.empty(0, dtype=tdt).element_size()
+    stride = n + (PAIR_GAP // es if layout == "padded" and k == 2 else 0)
+    slab = torch.empty((k - 1) * stride + n, dtype=tdt, device="cuda")
+    return [slab[j * stride:j * stride + n] for j in range(k)]
 
 
 def torch_dtype(dt):
@@ -392,7 +406,7 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
 
 
 def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None,
-                 n_devices=None, layout="one"):
+                 n_devices=None, layout="padded"):
     """One bucket of n_total elements split by element range over the ranks
     (mi_shard_range, 256-element aligned; BASELINE configs[3] as written):
     this rank reduces its shard of all k inputs.  `ins` (optional) holds
@@ -442,16 +456,13 @@ def config_legs(m, stream, layout, launches=10):
     from oneccl_amd import _lib
     legs = {}
     sh = stream.cuda_stream
-    other = "separate" if layout == "one" else "one"
-    c2_other = f"c2-layout-{other}"
-    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", c2_other):
-        desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if name == c2_other else name]
+    c2_other = {f"c2-layout-{x}": x for x in LAYOUTS if x != layout}  # the headline in the other layouts
+    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", *c2_other):
+        desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if name in c2_other else name]
         n = bucket // es
-        if name == c2_other:
-            # the headline's kernel and bucket in the other buffer layout
-            desc = (f"the headline (2-input fp32 sum, 1 GiB bucket) with acc and in "
-                    + ("in two allocations" if other == "separate" else "as the two halves of one allocation"))
-        ins = alloc_inputs(k, n, torch_dtype(dt), other if name == c2_other else layout)
+        if name in c2_other:
+            desc = f"the headline (2-input fp32 sum, 1 GiB bucket), layout: {LAYOUT_NOTE[c2_other[name]]}"
+        ins = alloc_inputs(k, n, torch_dtype(dt), c2_other.get(name, layout))
         for j, t in enumerate(ins):
             fill(t, 0xC0 + 131 * j)
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
@@ -475,7 +486,8 @@ def config_legs(m, stream, layout, launches=10):
         ceil = measured_ceiling(ins, k, n * es, stream)
         par = full_parity(lambda: _lib.check(step(), name), ins, k, dt, op, flags, 0xE0, "mi_reduce" if k == 2 else
                           "mi_reduce_multi")
-        legs[name] = {"workload": desc, "GiBps": round(bucket / GiB / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
+        legs[name] = {"workload": desc, "layout": LAYOUT_NOTE[c2_other.get(name, layout)],
+                      "GiBps": round(bucket / GiB / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
                       "roofline_frac": round(algo / (ms / 1e3) / (HBM_PEAK_GBPS * 1e9), 4),
                       "parity": {"elements": par["elements"], "mismatches": par["mismatches"]}}
         if ceil:
@@ -788,9 +800,7 @@ def main():
             "data": "synthetic (uniform [-1,1) generated on device)",
             "config": {"workload": desc, "bucket_bytes_per_gpu": units_per_rank, "inputs": k,
                        "layout": ("reduce_buf apart, the k - 1 peer chunks in one tmp allocation"
-                                  if args.config == "c4-tmpbuf" else
-                                  "the k inputs as consecutive slices of one allocation" if args.layout == "one"
-                                  else "one allocation per input"),
+                                  if args.config == "c4-tmpbuf" else LAYOUT_NOTE[args.layout]),
                        "op": ["sum", "prod", "min", "max"][op], "dtype_id": dt, "flags": flags,
                        "parallelism": f"element-range shard x{world}, no collective",
                        "entry": "mi_reduce (include/mi_reduce.h) via ctypes, async on the torch stream"},

@@ -16,6 +16,7 @@ One JSON line per trial, then a summary line.
 consecutive slices of one allocation; `nreduce` the accumulator alone and the
 other K - 1 inputs in one allocation, as oneCCL's nreduce lays out the peers'
 chunks in its tmp buffer (allreduce.cpp:333-394).
+--gap-mib G (layouts one / nreduce): G MiB between consecutive slices.
 --offsets (2 inputs): in each trial `in` is allocated 2 MiB larger and the
 same launch is timed with `in` shifted by 0, 4 KiB, 64 KiB and 1 MiB from its
 start, so the two operands' relative alignment changes while their pages do
@@ -41,6 +42,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--offsets", action="store_true")
     ap.add_argument("--layout", choices=("separate", "one", "nreduce"), default="separate")
+    ap.add_argument("--gap-mib", type=int, default=0)
     a = ap.parse_args()
     import torch
 
@@ -62,8 +64,9 @@ def main() -> None:
         else:
             first = 0 if a.layout == "one" else 1
             ins = [torch.empty(n, dtype=torch.float32, device="cuda").uniform_(-1, 1)] if first else []
-            slab = torch.empty((k - first) * n, dtype=torch.float32, device="cuda").uniform_(-1, 1)
-            ins += [slab[j * n:(j + 1) * n] for j in range(k - first)]
+            stride = n + (a.gap_mib << 18)
+            slab = torch.empty((k - first) * stride, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+            ins += [slab[j * stride:j * stride + n] for j in range(k - first)]
             del slab
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
 
@@ -86,11 +89,11 @@ def main() -> None:
         ts.sort()
         med = ts[len(ts) // 2]
         meds.append(med)
-        print(json.dumps({"trial": trial, "inputs": k, "layout": a.layout, "pad_MiB": pad_mib, "median_ms": round(med, 5),
+        print(json.dumps({"trial": trial, "inputs": k, "layout": a.layout, "gap_MiB": a.gap_mib, "pad_MiB": pad_mib, "median_ms": round(med, 5),
                           "best_ms": round(ts[0], 5), "TBps_median": round((k + 1) * (1 << 30) / med / 1e9, 3),
                           "addr_GiB": [round(t.data_ptr() / 2**30, 3) for t in ins]}), flush=True)
         del ins, arr, pad
-    print(json.dumps({"summary": True, "inputs": k, "layout": a.layout, "trials": a.trials, "min_ms": round(min(meds), 5),
+    print(json.dumps({"summary": True, "inputs": k, "layout": a.layout, "gap_MiB": a.gap_mib, "trials": a.trials, "min_ms": round(min(meds), 5),
                       "median_ms": round(statistics.median(meds), 5), "max_ms": round(max(meds), 5),
                       "spread": round(max(meds) / min(meds) - 1, 4),
                       "frac_of_8TBps_best": round((k + 1) * (1 << 30) / (min(meds) / 1e3) / 1e12 / 8.0, 4),
