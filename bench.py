@@ -98,7 +98,7 @@ LAYOUT_NOTE = {
 }
 
 
-def alloc_inputs(k, n, tdt, layout):
+def alloc_inputs(k, n, tdt, layout, device="cuda"):
     """The k input buffers of n elements.  Where the operands sit relative to
     each other decides the 2-input reduce's rate by up to 7 % (DESIGN.md §6,
     "Where the run-to-run spread comes from"): separate allocations draw a
@@ -110,10 +110,10 @@ def alloc_inputs(k, n, tdt, layout):
     no gap steadied); "one" is contiguous; "separate" is an allocation each."""
     import torch
     if layout == "separate":
-        return [torch.empty(n, dtype=tdt, device="cuda") for _ in range(k)]
+        return [torch.empty(n, dtype=tdt, device=device) for _ in range(k)]
     es = torch.empty(0, dtype=tdt).element_size()
     stride = n + (PAIR_GAP // es if layout == "padded" and k == 2 else 0)
-    slab = torch.empty((k - 1) * stride + n, dtype=tdt, device="cuda")
+    slab = torch.empty((k - 1) * stride + n, dtype=tdt, device=device)
     return [slab[j * stride:j * stride + n] for j in range(k)]
 
 

@@ -219,3 +219,28 @@ def test_device_identity_uses_pci_and_uuid_and_falls_back(monkeypatch):
     assert ids[0] == "0:11:0/abc" and ids[1] == "0:2f:0/def"
     assert ids[2] != ids[3] and ids[2].startswith("visible:")
     assert bench.device_plan(ids) == (4, 1, False)
+
+
+@pytest.mark.parametrize("layout,k,dtype", [("padded", 2, "float32"), ("padded", 2, "bfloat16"),
+                                            ("padded", 8, "float32"), ("one", 2, "float32"),
+                                            ("separate", 2, "float32")])
+def test_alloc_inputs_layouts(layout, k, dtype):
+    """The bench's input layouts: padded puts a 2-input
+    config's operands PAIR_GAP apart beyond the bucket in one allocation and
+    is contiguous for a fan-in; one is contiguous; separate is an allocation
+    each.  Checked on CPU tensors (the bench allocates on the GPU)."""
+    import torch
+    tdt = getattr(torch, dtype)
+    n = 1024
+    ins = bench.alloc_inputs(k, n, tdt, layout, device="cpu")
+    es = ins[0].element_size()
+    assert len(ins) == k and all(t.numel() == n and t.is_contiguous() for t in ins)
+    bases = [t.untyped_storage().data_ptr() for t in ins]
+    if layout == "separate":
+        assert len(set(bases)) == k
+        return
+    assert len(set(bases)) == 1  # one allocation
+    gap = bench.PAIR_GAP if layout == "padded" and k == 2 else 0
+    for j in range(1, k):
+        assert ins[j].data_ptr() - ins[j - 1].data_ptr() == n * es + gap
+    assert layout in bench.LAYOUTS and layout in bench.LAYOUT_NOTE
