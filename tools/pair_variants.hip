@@ -25,8 +25,12 @@
 //   pair_variants [trials=4] [launches=10]        one JSON line per pair x variant
 //   PAIR_RESIDENCY=1 pair_variants ...           the residency variants instead of the orders
 //   PAIR_WAVES=12,16,21 pair_variants ...        the library's order at these wave caps
+//   PAIR_SPLIT=1 pair_variants ...               acc and in loaded by different waves of a
+//                                                tile (through LDS), and read-only probes:
+//                                                both buffers per wave, or one per wave
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -89,6 +93,71 @@ __global__ __launch_bounds__(64) void fold2x2(f32x4* acc, const f32x4* in, uint6
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x1 + y1), rs, 1024u + threadIdx.x * 16u, 0, 18);
 }
 
+// two waves per tile: wave 0 brings acc's tile into LDS, wave 1 loads in's
+// and folds, so no wave reads both buffers
+__global__ __launch_bounds__(128) void fold2_split(f32x4* acc, const f32x4* in, uint64_t tiles) {
+    extern __shared__ f32x4 lds_tile[];
+    const uint64_t t = blockIdx.x;
+    const unsigned w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint64_t v = t * 64 + l;
+    f32x4 y = {0, 0, 0, 0};
+    if (w == 0)
+        lds_tile[l] = __builtin_nontemporal_load(acc + v);
+    else
+        y = __builtin_nontemporal_load(in + v);
+    __syncthreads();
+    if (w == 1) {
+        const f32x4 r = lds_tile[l] + y;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(acc + t * 64), (short)0,
+                                                                      1024, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, r), rs,
+                                               l * 16u, 0, 18);
+    }
+}
+
+// the same with two consecutive tiles per wave (as many loads in flight per
+// wave as the library's one-tile wave that loads both buffers)
+__global__ __launch_bounds__(128) void fold2_split2(f32x4* acc, const f32x4* in, uint64_t tiles) {
+    extern __shared__ f32x4 lds_tile[];
+    const uint64_t t = (uint64_t)blockIdx.x * 2;
+    const unsigned w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint64_t v = t * 64 + l;
+    f32x4 y0 = {0, 0, 0, 0}, y1 = {0, 0, 0, 0};
+    if (w == 0) {
+        lds_tile[l] = __builtin_nontemporal_load(acc + v);
+        lds_tile[64 + l] = __builtin_nontemporal_load(acc + v + 64);
+    } else {
+        y0 = __builtin_nontemporal_load(in + v);
+        y1 = __builtin_nontemporal_load(in + v + 64);
+    }
+    __syncthreads();
+    if (w == 1) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u4;
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(acc + t * 64), (short)0,
+                                                                      2048, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, lds_tile[l] + y0), rs, l * 16u, 0, 18);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, lds_tile[64 + l] + y1), rs, 1024u + l * 16u, 0,
+                                               18);
+    }
+}
+
+// reads only: both buffers per wave (ONE = false) or one buffer per wave,
+// alternate blocks taking acc and in (ONE = true)
+template <bool ONE>
+__global__ __launch_bounds__(64) void read2_probe(const f32x4* acc, const f32x4* in, uint64_t tiles, unsigned* sink) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    const uint64_t b = blockIdx.x;
+    f32x4 x;
+    if (ONE) {  // two consecutive tiles of one buffer: the same loads in flight per wave
+        const f32x4* p = ((b & 1) ? in : acc) + (b >> 1) * 128 + threadIdx.x;
+        x = __builtin_nontemporal_load(p) + __builtin_nontemporal_load(p + 64);
+    } else {
+        x = __builtin_nontemporal_load(acc + b * 64 + threadIdx.x) + __builtin_nontemporal_load(in + b * 64 + threadIdx.x);
+    }
+    if (x.x == 1234.5f && x.y == -1.0f) sink[threadIdx.x] = 1u;
+}
+
 __global__ void fill(float* p, uint64_t n, uint32_t seed) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t h = (uint32_t)i * 2654435761u ^ seed;
@@ -107,6 +176,8 @@ int main(int argc, char** argv) {
     std::vector<void*> pads;
     srand(7);
     float *chk_a, *chk_b;
+    unsigned* sink = nullptr;
+    CK(hipMalloc(&sink, 64 * sizeof(unsigned)));
     CK(hipMalloc(&chk_a, bytes));
     CK(hipMalloc(&chk_b, bytes));
     hipStream_t s;
@@ -135,6 +206,26 @@ int main(int argc, char** argv) {
                     break;
                 }
                 return (hipError_t)mi_reduce(in, acc, n, MI_FLOAT32, MI_OP_SUM, 0, s);
+            case 12: {
+                const unsigned gran2 = (unsigned)ldsb / 128u;
+                hipLaunchKernelGGL(fold2_split, g, dim3(128), std::max(1024u, (128u / 10u) * gran2), s, (f32x4*)acc,
+                                   (const f32x4*)in, tiles);
+                break;
+            }
+            case 13: {
+                const unsigned gran2 = (unsigned)ldsb / 128u;
+                hipLaunchKernelGGL(fold2_split2, dim3((unsigned)(tiles / 2)), dim3(128),
+                                   std::max(2048u, (128u / 10u) * gran2), s, (f32x4*)acc, (const f32x4*)in, tiles);
+                break;
+            }
+            case 14:
+                hipLaunchKernelGGL(read2_probe<false>, g, bl, lib_lds, s, (const f32x4*)acc, (const f32x4*)in, tiles,
+                                   sink);
+                break;
+            case 15:
+                hipLaunchKernelGGL(read2_probe<true>, g, bl, lib_lds, s, (const f32x4*)acc,
+                                   (const f32x4*)in, tiles, sink);
+                break;
             case 11:
                 hipLaunchKernelGGL(fold2x2, dim3((unsigned)(tiles / 2)), bl, lib_lds, s, (f32x4*)acc, (const f32x4*)in,
                                    tiles);
@@ -150,9 +241,13 @@ int main(int argc, char** argv) {
         }
         return hipGetLastError();
     };
-    const char* names[12] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
+    const char* names[16] = {"tile = block", "halves interleaved", "8 regions interleaved", "64 regions interleaved",
                              "in loaded first", "library (mi_reduce)", "walked backwards", "two windows from both ends",
-                             "16 waves/CU", "25 waves/CU", "no wave cap", "two tiles per wave"};
+                             "16 waves/CU", "25 waves/CU", "no wave cap", "two tiles per wave",
+                             "acc and in loaded by different waves (LDS)", "the same, two tiles per wave",
+                             "read both per wave (no store)",
+                             "read one buffer per wave (no store)"};
+    const bool split = getenv("PAIR_SPLIT") != nullptr;  // the split-wave fold and the read-only probes
     const bool resid = getenv("PAIR_RESIDENCY") != nullptr;  // time the residency variants instead of the orders
     std::vector<int> caps;  // PAIR_WAVES=12,16,21: the library's order at these caps instead
     if (const char* w = getenv("PAIR_WAVES"))
@@ -164,7 +259,7 @@ int main(int argc, char** argv) {
     auto name_of = [&](int v) { return v >= 100 ? std::to_string(v - 100) + " waves/CU" : std::string(names[v]); };
 
     // every variant's bits against the library's on one pair
-    for (int v : {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11}) {
+    for (int v : {0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13}) {
         CK(hipMemcpyAsync(chk_a, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(hipMemcpyAsync(chk_b, buf[0], bytes, hipMemcpyDeviceToDevice, s));
         CK(run(v, chk_a, buf[1]));
@@ -201,6 +296,7 @@ int main(int argc, char** argv) {
             for (int j = 0; j < 4; j++) {
                 if (i == j) continue;
                 std::vector<int> vs = resid ? std::vector<int>{5, 0, 8, 9, 10, 11} : std::vector<int>{5, 0, 1, 4, 6, 7};
+                if (split) vs = {5, 0, 12, 13, 14, 15};
                 if (!caps.empty()) {
                     vs = {5};
                     vs.insert(vs.end(), caps.begin(), caps.end());
