@@ -472,3 +472,45 @@ print("ok")
     env = dict(os.environ, MI_REDUCE_WAVE_CAP="0", PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("k,waves", [(2, 16), (2, 32), (2, 1), (8, 8), (8, 32), (0, 25)])
+def test_residency_override_same_bits(k, waves):
+    """mi_set_residency (tuning knob, tools/residency_ab.py) changes only the
+    LDS each one-wave workgroup reserves: the 2-input kernel, the fan-in and
+    the conversions give the oracle's bits at other residencies, and 0 puts
+    the plan back."""
+    m = _lib.mi()
+    w, lds = ctypes.c_int(), ctypes.c_uint()
+    _lib.check(m.mi_get_residency(0, k, ctypes.byref(w), None))
+    plan = w.value
+    n = 262144 + 5
+    try:
+        _lib.check(m.mi_set_residency(k, waves))
+        assert m.mi_get_residency(0, k, ctypes.byref(w), ctypes.byref(lds)) == 0 and w.value == waves
+        assert lds.value > 0
+        if k == 0:  # fp32 -> bf16 (RNE) conversion
+            a = rand_array(FP32, n, seed=77)
+            exp = oracle.f32_to_bf16(a, rne=True)
+            ta, pa = to_dev(a)
+            to, po = to_dev(np.zeros(n, dtype=np.uint16))
+            _lib.check(m.mi_convert(pa, FP32, po, BF16, n, F_BF16_RNE, _stream()))
+            _sync()
+            assert np.array_equal(from_dev(to, exp), exp)
+        elif k == 2:
+            a, b = rand_array(FP32, n, seed=78), rand_array(FP32, n, seed=79)
+            exp = b.copy()
+            oracle.comp_reduce(a, exp, FP32, 0, oracle.BF16_AVX512BF, oracle.FP16_AVX512F)
+            assert_same(gpu_reduce(a, b, FP32, 0, 0), exp, FP32, f"k=2 at {waves} waves")
+        else:
+            ins = [rand_array(FP32, n, seed=80 + j) for j in range(k)]
+            exp = oracle.fanin(ins, FP32, 0, oracle.BF16_AVX512BF, oracle.FP16_AVX512F)
+            holders = [to_dev(x) for x in ins]
+            to, po = to_dev(np.zeros_like(ins[0]))
+            arr = _lib.void_ptr_array([p for _, p in holders])
+            _lib.check(m.mi_reduce_multi(arr, k, po, n, FP32, 0, 0, _stream()))
+            _sync()
+            assert_same(from_dev(to, ins[0]), exp, FP32, f"k={k} at {waves} waves")
+    finally:
+        _lib.check(m.mi_set_residency(k, 0))
+    assert m.mi_get_residency(0, k, ctypes.byref(w), None) == 0 and w.value == plan
