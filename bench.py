@@ -69,8 +69,8 @@ def parse():
     p.add_argument("--no-config-legs", action="store_true",
                    help="skip the other BASELINE configs' legs (timed launches + full parity) of a c2 run")
     p.add_argument("--layout", default="padded", choices=LAYOUTS,
-                   help="padded (default): a config's inputs in one allocation, a 2-input config's operands "
-                        f"{PAIR_GAP >> 20} MiB apart beyond the bucket; one: consecutive slices of one allocation; "
+                   help="padded (default): a config's inputs in one allocation, a 2-input config's second operand "
+                        f"{PAIR_OFFSET >> 20} MiB after its first; one: consecutive slices of one allocation; "
                         "separate: one allocation per input (DESIGN.md §6, placement modes)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
@@ -90,9 +90,18 @@ def fill(t, seed):
 
 
 LAYOUTS = ("padded", "one", "separate")
-PAIR_GAP = 896 << 20  # bytes between the two operands of a padded layout
+PAIR_OFFSET = 1920 << 20  # where a padded layout's second operand starts, from the first
+PAIR_GAP = 896 << 20  # past the bucket, for a bucket larger than PAIR_OFFSET
+
+
+def pair_stride_bytes(nbytes):
+    """Offset of a padded layout's second operand from its first."""
+    return PAIR_OFFSET if nbytes <= PAIR_OFFSET else nbytes + PAIR_GAP
+
+
 LAYOUT_NOTE = {
-    "padded": f"the inputs in one allocation; a 2-input config's operands {PAIR_GAP >> 20} MiB apart beyond the bucket",
+    "padded": f"the inputs in one allocation; a 2-input config's second operand {PAIR_OFFSET >> 20} MiB after the "
+              f"first (buckets up to that size; larger: {PAIR_GAP >> 20} MiB past the bucket)",
     "one": "the inputs as consecutive slices of one allocation",
     "separate": "one allocation per input",
 }
@@ -105,14 +114,15 @@ def alloc_inputs(k, n, tdt, layout, device="cuda"):
     placement per run (fast, medium or slow: 0.471-0.511 ms for C2); slices of
     one allocation run at one rate whose level follows their offset (C2: 0.480
     ms at 1 GiB, 0.473-0.475 at 1 GiB + 896 MiB on two boxes,
-    profiles/round4_run7/).  "padded" puts a 2-input config's operands
-    PAIR_GAP apart beyond the bucket and is contiguous for a fan-in (whose rate
-    no gap steadied); "one" is contiguous; "separate" is an allocation each."""
+    profiles/round4_run7/; 256 MiB operands likewise, profiles/round4_run12/).
+    "padded" starts a 2-input config's second operand PAIR_OFFSET after its
+    first (pair_stride_bytes) and is contiguous for a fan-in (whose rate no gap
+    steadied); "one" is contiguous; "separate" is an allocation each."""
     import torch
     if layout == "separate":
         return [torch.empty(n, dtype=tdt, device=device) for _ in range(k)]
     es = torch.empty(0, dtype=tdt).element_size()
-    stride = n + (PAIR_GAP // es if layout == "padded" and k == 2 else 0)
+    stride = pair_stride_bytes(n * es) // es if layout == "padded" and k == 2 else n
     slab = torch.empty((k - 1) * stride + n, dtype=tdt, device=device)
     return [slab[j * stride:j * stride + n] for j in range(k)]
 

@@ -225,8 +225,8 @@ def test_device_identity_uses_pci_and_uuid_and_falls_back(monkeypatch):
                                             ("padded", 8, "float32"), ("one", 2, "float32"),
                                             ("separate", 2, "float32")])
 def test_alloc_inputs_layouts(layout, k, dtype):
-    """The bench's input layouts: padded puts a 2-input
-    config's operands PAIR_GAP apart beyond the bucket in one allocation and
+    """The bench's input layouts: padded starts a 2-input
+    config's second operand PAIR_OFFSET after its first in one allocation and
     is contiguous for a fan-in; one is contiguous; separate is an allocation
     each.  Checked on CPU tensors (the bench allocates on the GPU)."""
     import torch
@@ -240,7 +240,10 @@ def test_alloc_inputs_layouts(layout, k, dtype):
         assert len(set(bases)) == k
         return
     assert len(set(bases)) == 1  # one allocation
-    gap = bench.PAIR_GAP if layout == "padded" and k == 2 else 0
+    stride = bench.PAIR_OFFSET if layout == "padded" and k == 2 else n * es
     for j in range(1, k):
-        assert ins[j].data_ptr() - ins[j - 1].data_ptr() == n * es + gap
+        assert ins[j].data_ptr() - ins[j - 1].data_ptr() == stride
+    # a bucket larger than the offset: the gap past it
+    assert bench.pair_stride_bytes(bench.PAIR_OFFSET + 16) == bench.PAIR_OFFSET + 16 + bench.PAIR_GAP
+    assert bench.pair_stride_bytes(1 << 30) == bench.PAIR_OFFSET
     assert layout in bench.LAYOUTS and layout in bench.LAYOUT_NOTE

@@ -17,6 +17,7 @@ consecutive slices of one allocation; `nreduce` the accumulator alone and the
 other K - 1 inputs in one allocation, as oneCCL's nreduce lays out the peers'
 chunks in its tmp buffer (allreduce.cpp:333-394).
 --gap-mib G (layouts one / nreduce): G MiB between consecutive slices.
+--bucket-mib B: each input B MiB of fp32 (default 1024).
 --offsets (2 inputs): in each trial `in` is allocated 2 MiB larger and the
 same launch is timed with `in` shifted by 0, 4 KiB, 64 KiB and 1 MiB from its
 start, so the two operands' relative alignment changes while their pages do
@@ -43,13 +44,15 @@ def main() -> None:
     ap.add_argument("--offsets", action="store_true")
     ap.add_argument("--layout", choices=("separate", "one", "nreduce"), default="separate")
     ap.add_argument("--gap-mib", type=int, default=0)
+    ap.add_argument("--bucket-mib", type=int, default=1024, help="bytes per input (fp32)")
     a = ap.parse_args()
     import torch
 
     from oneccl_amd import _lib
     m = _lib.mi()
     s = torch.cuda.current_stream()
-    n = (1 << 30) // 4
+    n = (a.bucket_mib << 20) // 4
+    nb = n * 4
     k = a.inputs
     rng = random.Random(a.seed)
     meds = []
@@ -90,14 +93,14 @@ def main() -> None:
         med = ts[len(ts) // 2]
         meds.append(med)
         print(json.dumps({"trial": trial, "inputs": k, "layout": a.layout, "gap_MiB": a.gap_mib, "pad_MiB": pad_mib, "median_ms": round(med, 5),
-                          "best_ms": round(ts[0], 5), "TBps_median": round((k + 1) * (1 << 30) / med / 1e9, 3),
+                          "best_ms": round(ts[0], 5), "TBps_median": round((k + 1) * nb / med / 1e9, 3),
                           "addr_GiB": [round(t.data_ptr() / 2**30, 3) for t in ins]}), flush=True)
         del ins, arr, pad
     print(json.dumps({"summary": True, "inputs": k, "layout": a.layout, "gap_MiB": a.gap_mib, "trials": a.trials, "min_ms": round(min(meds), 5),
                       "median_ms": round(statistics.median(meds), 5), "max_ms": round(max(meds), 5),
                       "spread": round(max(meds) / min(meds) - 1, 4),
-                      "frac_of_8TBps_best": round((k + 1) * (1 << 30) / (min(meds) / 1e3) / 1e12 / 8.0, 4),
-                      "frac_of_8TBps_worst": round((k + 1) * (1 << 30) / (max(meds) / 1e3) / 1e12 / 8.0, 4)}),
+                      "frac_of_8TBps_best": round((k + 1) * nb / (min(meds) / 1e3) / 1e12 / 8.0, 4),
+                      "frac_of_8TBps_worst": round((k + 1) * nb / (max(meds) / 1e3) / 1e12 / 8.0, 4)}),
           flush=True)
 
 
