@@ -54,6 +54,11 @@ int mi_ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, int u
 int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
 /* ccl_fp16_reduce, src/comp/fp16/fp16.cpp:41-53 */
 int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
+/* ccl_bf16_reduce_host / ccl_fp16_reduce_host (mi_ccl_lp_host.hpp): the MPI
+ * user ops' reduce (atl_mpi_ctx.cpp:57-63, 87-92, integration/0002), host
+ * memory by construction: no pointer lookup up to the CPU threshold */
+int mi_ccl_bf16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
+int mi_ccl_fp16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op);
 /* ccl_convert_fp32_to_bf16_arrays / ccl_convert_bf16_to_fp32_arrays,
  * src/comp/bf16/bf16.cpp:113-169 (rounding per the bf16 impl type) */
 int mi_ccl_convert_fp32_to_bf16_arrays(void* fp32_buf, void* bf16_buf, size_t count);

@@ -101,6 +101,8 @@ SHIM_API = [
     ("mi_ccl_comp_copy_host", c_int, [c_void_p, c_void_p, c_size_t, c_int]),
     ("mi_ccl_bf16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
     ("mi_ccl_fp16_reduce", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
+    ("mi_ccl_bf16_reduce_host", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
+    ("mi_ccl_fp16_reduce_host", c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_size_t), c_int]),
     ("mi_ccl_convert_fp32_to_bf16_arrays", c_int, [c_void_p, c_void_p, c_size_t]),
     ("mi_ccl_convert_bf16_to_fp32_arrays", c_int, [c_void_p, c_void_p, c_size_t]),
     ("mi_ccl_convert_fp32_to_fp16", c_int, [c_void_p, c_void_p]),

@@ -8,6 +8,7 @@
 //   ccl_reduction_to_str    src/comp/comp.cpp:251-260
 //   ccl_bf16_reduce         src/comp/bf16/bf16.cpp:87-110
 //   ccl_fp16_reduce         src/comp/fp16/fp16.cpp:41-53
+//   ccl_{bf16,fp16}_reduce_host  the MPI user ops' call, atl_mpi_ctx.cpp:57-63,87-92
 //   bf16_impl_names / fp16_impl_names / fp16_env_impl_names (bf16.cpp:26-30, fp16.cpp:25-39)
 // Which bit-level behaviour the reference would show (bf16 truncation vs
 // RNE, min/max operand order) is taken from the same place the reference
@@ -53,6 +54,7 @@
 #define MI_LOG_DEBUG(...) LOG_DEBUG(__VA_ARGS__)
 #include "mi_ccl_comp.h"  // include/ (on the include path)
 #include "mi_ccl_comp_async.hpp"
+#include "mi_ccl_lp_host.hpp"
 static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
 static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
 // CCL_COMP_HIP_DEVICE: the GPU for operands that name none (host buffers);
@@ -100,6 +102,7 @@ static void mi_log_debug(int line, const char* fn, const A&... a) {
 }
 #define MI_CCL_FATAL(msg) mi_ccl_fatal(msg)
 #include "../../include/mi_ccl_comp_async.hpp"
+#include "../../include/mi_ccl_lp_host.hpp"
 #endif
 
 // bf16.cpp:26-30, fp16.cpp:25-39 — referenced by env.cpp:711-720, 1101-1102
@@ -368,6 +371,9 @@ bool host_schedule(const ccl_sched* sched) { return sched && !sched->coll_param.
 struct SchedScope {
     const bool prev;
     explicit SchedScope(const ccl_sched* sched) : prev(t_host_by_sched) { t_host_by_sched = host_schedule(sched); }
+    // a caller whose operands are host memory by construction (the MPI user
+    // ops, include/mi_ccl_lp_host.hpp) gives the same word without a schedule
+    explicit SchedScope(bool host) : prev(t_host_by_sched) { t_host_by_sched = host; }
     ~SchedScope() { t_host_by_sched = prev; }
 };
 
@@ -960,6 +966,22 @@ void ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t*
     check(reduce2_sync(in_buf, inout_buf, in_cnt, MI_FLOAT16, static_cast<int>(op), f), "mi_reduce_sync(fp16)");
 }
 
+// The MPI user ops' reduce (include/mi_ccl_lp_host.hpp, integration/0002):
+// bf16_base_op and fp16_base_op (atl_mpi_ctx.cpp:57-63, 87-92) fold MPI's own
+// host buffers, so their word is the one a schedule without a stream gives
+// (comp.cpp:136-142): a bucket up to the dispatcher's threshold goes to the
+// calling thread's CPU with nothing looked up (host_kind -> kHostBySched);
+// a larger one is looked up once to pick the GPU's pinned or staged route.
+void ccl_bf16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
+    const SchedScope scope(true);
+    ccl_bf16_reduce(in_buf, in_cnt, inout_buf, out_cnt, op);
+}
+
+void ccl_fp16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, ccl::reduction op) {
+    const SchedScope scope(true);
+    ccl_fp16_reduce(in_buf, in_cnt, inout_buf, out_cnt, op);
+}
+
 // ---- conversions: bf16.cpp:113-169, fp16.cpp:55-61 ------------------------
 // ccl_convert_fp32_to_bf16_arrays: non-scalar impls convert (count/16)*16
 // elements with the impl's rounding (avx512bf RNE, avx512f truncate) and
@@ -1362,6 +1384,20 @@ int mi_ccl_bf16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_
 int mi_ccl_fp16_reduce(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
     MI_SHIM_GUARD({
         ccl_fp16_reduce(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
+        return 0;
+    });
+}
+
+int mi_ccl_bf16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
+    MI_SHIM_GUARD({
+        ccl_bf16_reduce_host(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
+        return 0;
+    });
+}
+
+int mi_ccl_fp16_reduce_host(const void* in_buf, size_t in_cnt, void* inout_buf, size_t* out_cnt, int op) {
+    MI_SHIM_GUARD({
+        ccl_fp16_reduce_host(in_buf, in_cnt, inout_buf, out_cnt, static_cast<ccl::reduction>(op));
         return 0;
     });
 }

@@ -75,6 +75,16 @@ def test_shim_exports_async_entry_points():
         assert w in out, w
 
 
+def test_shim_exports_mpi_user_op_host_entries():
+    """The MPI user ops' host-word entries (include/mi_ccl_lp_host.hpp,
+    integration/0002), with ccl_bf16_reduce's signature."""
+    out = subprocess.run(["nm", "-DC", "--defined-only", str(ROOT / "oneccl_amd/lib/libccl_comp_hip.so")],
+                         check=True, capture_output=True, text=True).stdout
+    for name in ("ccl_bf16_reduce_host", "ccl_fp16_reduce_host"):
+        w = f"{name}(void const*, unsigned long, void*, unsigned long*, ccl::v1::reduction)"
+        assert w in out, w
+
+
 def test_async_empty_reduce_needs_no_device():
     """in_count == 0 completes inside start without touching HIP
     (comp.cpp:132-134); a null request pointer is an error."""

@@ -12,7 +12,7 @@ the drop-in's in-tree object.  Copies go to a temporary directory; the
 reference tree is only read.  Runs where /root/reference exists.
 
   0001  src/CMakeLists.txt        swap three src/comp sources, link libmi_reduce.so  (§2a)
-  0002  atl_mpi_ctx.cpp           MPI fp16 user op through ccl_fp16_reduce          (§2b)
+  0002  atl_mpi_ctx.cpp           MPI bf16/fp16 user ops through the host-word entries (§2b)
   0003  reduce_local_entry, recv_reduce_entry: start the reduce, poll it        (§2d)
   0004  allreduce.cpp nreduce + entry_factory.hpp: one fused fan-in per segment (§2e)
   0005  buffer_cache.cpp: the regular buffer cache declares its host buffers     (§2h)
@@ -140,9 +140,14 @@ def test_patched_units_need_only_what_the_dropin_defines(objs):
     # the schedule reaches the asynchronous entries (its stream decides
     # whether operands are looked up): ccl_sched* is their first parameter
     assert all("P9ccl_sched" in s for s in starts), starts
-    fp16 = {s for s in _undefs(objs["atl_mpi_ctx"][0]) if "fp16" in s}
-    assert any("ccl_fp16_reduce" in s for s in fp16)
+    mpi = _undefs(objs["atl_mpi_ctx"][0])
+    fp16 = {s for s in mpi if "fp16" in s}
     assert not any("wrap" in s for s in fp16), fp16  # the inline SIMD body is no longer used
+    # 0002: both MPI user ops say their operands are host memory
+    # (include/mi_ccl_lp_host.hpp), so a small bucket is folded with no lookup
+    assert any(s.startswith("_Z20ccl_fp16_reduce_host") for s in mpi), sorted(fp16)
+    assert any(s.startswith("_Z20ccl_bf16_reduce_host") for s in mpi), sorted(mpi)
+    assert not any(re.match(r"_Z15ccl_(bf16|fp16)_reduce", s) for s in mpi), sorted(mpi)
 
 
 def test_buffer_cache_declares_exactly_what_it_frees(tree, objs):

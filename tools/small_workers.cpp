@@ -15,12 +15,22 @@
 //   copyhost ccl_comp_copy_host, the copy entries' call after
 //            integration/0006 (host to host, nothing looked up)
 //   memcpy   plain memcpy: the reference's ccl_comp_copy (comp.cpp:60-74)
+// The MPI user ops (atl_mpi_ctx.cpp:57-63, 87-92; bf16/fp16 sum, elements of
+// 2 bytes):
+//   mpibf16 / mpifp16  ccl_{bf16,fp16}_reduce_host, integration/0002's call:
+//            host memory by the caller's word, nothing looked up
+//   bf16 / fp16        ccl_{bf16,fp16}_reduce with no word (every operand
+//            looked up): the user ops' call before that patch
+//   refbf16 / reffp16  the reference's own AVX-512 body (avx512bf /
+//            avx512f impl) from oracle/_ref/libref_comp.so: what the user
+//            op runs in the reference (bf16.cpp:98-109, fp16_intrisics.hpp:204)
 // Also prints the HIP pointer lookups the drop-in made per call.
 #include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -30,16 +40,29 @@
 #include "mi_ccl_comp.h"
 
 typedef int (*ref_reduce_t)(const void*, size_t, void*, size_t*, int, size_t, int);
+typedef int (*ref_lp_t)(int, int, const uint16_t*, uint16_t*, size_t);
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: small_workers T [elements] [default|reg|sched|ref]\n");
+        fprintf(stderr, "usage: small_workers T [elements] [mode]\n");
         return 2;
     }
     const int T = atoi(argv[1]);
     const size_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 1024;
     const std::string mode = argc > 3 ? argv[3] : "default";
     ref_reduce_t ref = nullptr;
+    ref_lp_t ref_lp = nullptr;
+    const bool lp = mode.find("bf16") != std::string::npos || mode.find("fp16") != std::string::npos;
+    const size_t es = lp ? 2 : sizeof(float);
+    if (mode == "refbf16" || mode == "reffp16") {
+        const char* path = getenv("REF_LP_SO") ? getenv("REF_LP_SO") : "oracle/_ref/libref_comp.so";
+        void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+        const char* sym = mode == "refbf16" ? "ref_bf16_reduce" : "ref_fp16_reduce";
+        if (!h || !(ref_lp = (ref_lp_t)dlsym(h, sym))) {
+            fprintf(stderr, "cannot load %s: %s\n", path, dlerror());
+            return 2;
+        }
+    }
     if (mode == "ref") {
         const char* path = getenv("REF_COMP_SO") ? getenv("REF_COMP_SO") : "oracle/_ref/libref_ccl_comp.so";
         void* h = dlopen(path, RTLD_LAZY | RTLD_LOCAL);
@@ -56,6 +79,9 @@ int main(int argc, char** argv) {
     for (int t = 0; t < T; t++)
         th.emplace_back([&, t] {
             std::vector<float> a(n, 1.f), b(n, 1.f);
+            // 2-byte modes: bf16 1.0 (0x3f80) / fp16 1.0 (0x3c00), n elements
+            const uint16_t one = mode.find("bf16") != std::string::npos ? 0x3f80 : 0x3c00;
+            std::vector<uint16_t> a2(lp ? n : 0, one), b2(lp ? n : 0, one);
             if (mode == "reg") {
                 mi_ccl_comp_register_host_buffer(a.data(), n * sizeof(float));
                 mi_ccl_comp_register_host_buffer(b.data(), n * sizeof(float));
@@ -64,6 +90,11 @@ int main(int argc, char** argv) {
             const size_t nb = n * sizeof(float);
             auto call = [&] {
                 if (ref) ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0);
+                else if (ref_lp) ref_lp(mode == "refbf16" ? 2 : 3, 0, a2.data(), b2.data(), n);
+                else if (mode == "mpibf16") mi_ccl_bf16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
+                else if (mode == "mpifp16") mi_ccl_fp16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
+                else if (mode == "bf16") mi_ccl_bf16_reduce(a2.data(), n, b2.data(), nullptr, 0);
+                else if (mode == "fp16") mi_ccl_fp16_reduce(a2.data(), n, b2.data(), nullptr, 0);
                 else if (mode == "copy") mi_ccl_comp_copy(a.data(), b.data(), nb, 0);
                 else if (mode == "copyhost") mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0);
                 else if (mode == "memcpy") memcpy(b.data(), a.data(), nb);
@@ -90,6 +121,6 @@ int main(int argc, char** argv) {
     const bool roctx_on = mi ? strcmp(mi, "0") != 0 : (itt && atoi(itt) > 0);
     printf("{\"mode\": \"%s%s\", \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
            "\"max_us\": %.3f, \"lookups_per_call\": %.2f, \"iters\": %ld}\n",
-           mode.c_str(), roctx_on ? " (roctx on)" : "", T, n, n * sizeof(float), s[T / 2], s[T - 1], lk, iters);
+           mode.c_str(), roctx_on ? " (roctx on)" : "", T, n, n * es, s[T / 2], s[T - 1], lk, iters);
     fflush(stdout);
 }
