@@ -283,11 +283,15 @@ int mi_pointer_kind_range(const void* ptr, size_t bytes, int* device);
  * entry point then classifies an operand lying wholly inside a declared
  * range without asking HIP (readers take no lock).  mi_host_declare looks
  * the range up once (both ends): device or managed memory is refused with
- * MI_E_INVALID, as is a range mixing kinds; pinned ranges stay pinned (the
- * zero-copy path), pageable ones pageable.  Declare after any
- * mi_host_register of the same buffer.  Ranges may not overlap.  Undeclare
- * (by the start address) before the memory is freed; a range must not be
- * undeclared while a reduce on it is in flight.  oneCCL's
+ * MI_E_INVALID, as is a range mixing kinds.  A pinned range is recorded as
+ * pinned (the zero-copy path) only when it lies inside one pinned
+ * allocation (one mi_host_register, or the allocation HIP reports for it);
+ * otherwise it is recorded as pageable (staged), since pinned ends do not
+ * make the pages between them pinned.  Declare after any mi_host_register of
+ * the same buffer; mi_host_unregister turns the declared ranges over the
+ * buffer pageable before unpinning it.  Ranges may not overlap.  Undeclare
+ * (by the start address) before the memory is freed or unpinned by other
+ * means; a range must not be undeclared while a reduce on it is in flight.  oneCCL's
  * regular_buffer_cache declares its buffers (integration/0005, INTEGRATION.md
  * §2f; the place it registers them with Level Zero,
  * src/sched/buffer/buffer_cache.cpp:99-104).                               */

@@ -382,6 +382,29 @@ bool is_device_ptr(const void* p) {
     return mi_pointer_kind(p, &dev) == 0;
 }
 
+// The host word, checked.  A caller that says its operands are host memory
+// (a schedule without a stream, the MPI user ops, the copy entries) has them
+// dereferenced on the CPU, as the reference does; device memory passed there
+// would fault the host instead of being detected.  Under CCL_COMP_CHECK_HOST=1
+// (or CCL_LOG_LEVEL=debug|trace) such operands are classified anyway and
+// device memory fails loudly (CCL_THROW).  Read once.
+bool check_host_word() {
+    static const bool on = [] {
+        if (const char* v = getenv("CCL_COMP_CHECK_HOST")) return strcmp(v, "0") != 0;
+        const char* l = getenv("CCL_LOG_LEVEL");
+        return l && (strcmp(l, "debug") == 0 || strcmp(l, "trace") == 0);
+    }();
+    return on;
+}
+
+void verify_host_word(const void* const* ptrs, int n, const char* what) {
+    if (!check_host_word()) return;
+    for (int i = 0; i < n; i++)
+        if (ptrs[i] && is_device_ptr(ptrs[i]))
+            MI_CCL_THROW(std::string(what) + ": device memory passed where the caller says host memory "
+                         "(a collective without a stream, an MPI user op or a host copy entry)");
+}
+
 // reference behaviour for a user callback (comp.cpp:84-88); device operands
 // are staged through host memory, as the reference's SYCL branch does
 // (comp.cpp:136-195)
@@ -390,6 +413,10 @@ void run_custom(const void* in_buf, size_t in_count, void* inout_buf, size_t* ou
     if (!fn) MI_CCL_THROW("custom reduction requires user callback");
     // host memory by the schedule's word: straight to the callback, as the
     // reference does (comp.cpp:139-142)
+    if (t_host_by_sched) {
+        const void* ops[2] = {in_buf, inout_buf};
+        verify_host_word(ops, 2, "custom reduce");
+    }
     const bool din = !t_host_by_sched && is_device_ptr(in_buf), dio = !t_host_by_sched && is_device_ptr(inout_buf);
     if (!din && !dio) {
         fn(in_buf, in_count, inout_buf, out_count, dtype.idx(), context);
@@ -513,7 +540,14 @@ int host_kind(const void* const* ptrs, int n, const void* out, size_t bytes = 0)
         // path whatever its pointer kinds needs no lookup at all; above
         // that the kinds still pick pinned zero-copy or staging
         const HostMax m = mi_host_max();
-        if (m.pageable > 0 && m.pinned > 0 && bytes <= std::min(m.pageable, m.pinned)) return kHostBySched;
+        if (m.pageable > 0 && m.pinned > 0 && bytes <= std::min(m.pageable, m.pinned)) {
+            if (check_host_word()) {
+                verify_host_word(&out, 1, "reduce");
+                for (int i = 0; i < n; i++)
+                    if (ptrs[i] != out) verify_host_word(&ptrs[i], 1, "reduce");
+            }
+            return kHostBySched;
+        }
     }
     int kind = pointer_kind(out, bytes);
     if (kind == 0) return 0;
@@ -938,6 +972,8 @@ ccl::status ccl_comp_copy_host(const void* in_buf, void* out_buf, size_t bytes, 
     if (!out_buf) MI_CCL_THROW("out_buf is null");
     MI_LOG_DEBUG("copy: bytes ", bytes, ", operands: host memory by the copy entry (not looked up), path: cpu",
                  use_nontemporal ? " (non-temporal)" : "");
+    const void* ops[2] = {in_buf, out_buf};
+    verify_host_word(ops, 2, "copy");
     check(mi_thread_sync(), "mi_thread_sync");
     check(mi_host_copy(out_buf, in_buf, bytes, use_nontemporal ? 1 : 0), "mi_host_copy");
     return ccl::status::success;

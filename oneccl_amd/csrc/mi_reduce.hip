@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
+#include <map>
 #include <memory>
 #include <thread>
 #include <cstdlib>
@@ -404,6 +405,9 @@ struct ReaderSlotRef {  // the calling thread's slot, released when it exits
     int idx = -2;       // -2: not taken yet, -1: none free (read under the mutex)
     ~ReaderSlotRef() {
         if (idx >= 0) g_readers[idx].used.store(false, std::memory_order_release);
+        // a read later in this thread's exit (another thread_local's
+        // destructor) takes the mutex path: the slot may be another thread's now
+        idx = -1;
     }
 };
 thread_local ReaderSlotRef t_reader;
@@ -2064,15 +2068,100 @@ const char* mi_reduction_to_str(int op) {
     }
 }
 
+// ---- pinned extents --------------------------------------------------------
+// A declared range is recorded as pinned only when it lies inside one pinned
+// allocation: its two ends being pinned does not make its middle pinned, and
+// a kernel reading pageable pages in place faults the GPU (no XNACK).  The
+// allocation is the one mi_host_register pinned, or the one HIP reports for
+// the address (hipHostMalloc / a caller's own hipHostRegister).  Anything
+// else is recorded as pageable, which is always safe: it is staged.
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_registered;  // mi_host_register: base -> bytes, under g_reg_mu
+
+bool registered_extent(uintptr_t a, uintptr_t* lo, uintptr_t* hi) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_registered.upper_bound(a);
+    if (it == g_registered.begin()) return false;
+    --it;
+    if (a - it->first >= it->second) return false;
+    *lo = it->first;
+    *hi = it->first + it->second;
+    return true;
+}
+
+// [lo, hi): the pinned allocation holding host address a, whose device-visible
+// address is a + delta
+bool pinned_extent(uintptr_t a, intptr_t delta, uintptr_t* lo, uintptr_t* hi) {
+    if (registered_extent(a, lo, hi)) return true;
+    void* start = nullptr;
+    size_t size = 0;
+    hipDeviceptr_t q = reinterpret_cast<hipDeviceptr_t>(a + delta);
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, q) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, q) != hipSuccess || size == 0) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t st = reinterpret_cast<uintptr_t>(start);
+    for (const uintptr_t base : {st, st - (uintptr_t)delta})  // host or device-visible answer
+        if (base <= a && a - base < size) {
+            *lo = base;
+            *hi = base + size;
+            return true;
+        }
+    return false;
+}
+
+// Declared pinned ranges overlapping [lo, hi) become pageable (staged from
+// then on): the memory under them is about to be unpinned.
+void demote_declared(uintptr_t lo, uintptr_t hi) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    const RangeSnap* cur = g_rng.load(std::memory_order_relaxed);
+    if (!cur) return;
+    bool any = false;
+    for (const HostRange& r : cur->r) any |= r.kind == PK_PINNED && r.lo < hi && lo < r.hi;
+    if (!any) return;
+    std::unique_ptr<RangeSnap> next(new RangeSnap(*cur));
+    for (HostRange& r : next->r)
+        if (r.kind == PK_PINNED && r.lo < hi && lo < r.hi) {
+            r.kind = PK_PAGEABLE;
+            r.dev_delta = 0;
+        }
+    publish_ranges(next.release());
+}
+
 int mi_host_register(void* ptr, size_t bytes) {
     if (!ptr || !bytes) return fail(MI_E_INVALID, "null / empty buffer");
     MI_HIP(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    try {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_registered[reinterpret_cast<uintptr_t>(ptr)] = bytes;
+    } catch (const std::exception&) {
+        (void)hipHostUnregister(ptr);
+        return fail(MI_E_RESOURCE, "out of memory");
+    }
     return 0;
 }
 
 int mi_host_unregister(void* ptr) {
     if (!ptr) return fail(MI_E_INVALID, "null buffer");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    uintptr_t lo = a, hi = a + 1;
+    size_t known = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_registered.find(a);
+        if (it != g_registered.end()) known = it->second;
+    }
+    if (known) hi = a + known;
+    else if (!pinned_extent(a, 0, &lo, &hi)) hi = a + 1;  // extent unknown: the ranges at ptr
+    try {
+        demote_declared(lo, hi);  // before the pages are unpinned
+    } catch (const std::exception&) {
+        return fail(MI_E_RESOURCE, "out of memory");
+    }
     MI_HIP(hipHostUnregister(ptr));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_registered.erase(a);
     return 0;
 }
 
@@ -2107,6 +2196,11 @@ int mi_host_declare(const void* ptr, size_t bytes) {
     const intptr_t delta = (intptr_t)(reinterpret_cast<uintptr_t>(v0) - a);
     if (k0 == PK_PINNED && (intptr_t)(reinterpret_cast<uintptr_t>(v1) - last) != delta)
         return fail(MI_E_INVALID, "the pinned range spans several mappings");
+    PtrKind kind = k0;
+    if (kind == PK_PINNED) {  // pinned in place only inside one pinned allocation
+        uintptr_t lo = 0, hi = 0;
+        if (!pinned_extent(a, delta, &lo, &hi) || bytes > hi - a) kind = PK_PAGEABLE;
+    }
     try {
         std::lock_guard<std::mutex> lk(g_rng_mu);
         const RangeSnap* cur = g_rng.load(std::memory_order_relaxed);
@@ -2116,7 +2210,7 @@ int mi_host_declare(const void* ptr, size_t bytes) {
                                    [](uintptr_t x, const HostRange& r) { return x < r.lo; });
         if (it != next->r.end() && it->lo < a + bytes) return fail(MI_E_INVALID, "overlaps a declared range");
         if (it != next->r.begin() && std::prev(it)->hi > a) return fail(MI_E_INVALID, "overlaps a declared range");
-        next->r.insert(it, HostRange{a, a + bytes, k0, k0 == PK_PINNED ? delta : 0});
+        next->r.insert(it, HostRange{a, a + bytes, kind, kind == PK_PINNED ? delta : 0});
         publish_ranges(next.release());
         g_rng_n.fetch_add(1, std::memory_order_release);
     } catch (const std::exception&) {

@@ -15,6 +15,7 @@
 
 #include "../../oneccl_amd/csrc/ccl_mirror.hpp"
 #include "../../include/mi_ccl_comp_async.hpp"
+#include "../../include/mi_ccl_lp_host.hpp"
 
 // reduce_local_entry as INTEGRATION.md §2(d) patches it: start() issues the
 // reduce and returns `started`; the worker's progress loop calls update()
@@ -50,17 +51,17 @@ struct async_reduce_entry {
 };
 
 // MPI user ops (MPI_User_function shape) as src/atl/mpi/atl_mpi_ctx.cpp
-// registers them: bf16_sum_op -> ccl_bf16_reduce(in, *length, inout, nullptr,
-// op) (:87-100, unchanged), and the fp16 op with INTEGRATION.md §2b applied
-// (:58-64, ccl_fp16_reduce instead of the inline CPU body).  MPI calls them
-// from its own progress thread on host buffers.
+// registers them, with integration/0002 applied: bf16_base_op (:87-92) and
+// fp16_base_op (:57-63) call ccl_{bf16,fp16}_reduce_host, whose operands are
+// host memory by the caller's word (include/mi_ccl_lp_host.hpp).  MPI calls
+// them from its own progress thread on host buffers.
 typedef void (*mpi_user_fn)(void* in, void* inout, int* length, void* datatype);
 static void bf16_sum_op(void* in, void* inout, int* length, void*) {
-    ccl_bf16_reduce(in, *length, inout, nullptr, ccl::reduction::sum);
+    ccl_bf16_reduce_host(in, *length, inout, nullptr, ccl::reduction::sum);
 }
 static void fp16_max_op(void* in, void* inout, int* length, void*) {
     size_t len = *length;
-    ccl_fp16_reduce(in, len, inout, nullptr, ccl::reduction::max);
+    ccl_fp16_reduce_host(in, len, inout, nullptr, ccl::reduction::max);
 }
 
 static int failures = 0;

@@ -6,6 +6,10 @@
 // the whole run (must always see kind 2, pageable), and short-lived reader
 // threads (slot recycling).  Writers: threads that declare and undeclare
 // ranges of their own in a loop (snapshot publication + grace periods).
+// Exiting readers: threads whose last read happens inside a thread_local
+// destructor that runs after the library has released the thread's reader
+// slot: that read must take the locked path, not a slot another
+// thread may own.
 // Exit 0 when every check held.  No GPU is needed: undeclared pointers are
 // classified by HIP, which reports pageable (or no device) on a CPU host.
 #include <atomic>
@@ -16,6 +20,17 @@
 #include <vector>
 
 #include "../../include/mi_reduce.h"
+
+// Constructed before the thread's first classification, so destroyed after
+// the library's own thread_local slot reference: its read is a late one.
+struct LateReader {
+    const unsigned char* p = nullptr;
+    std::atomic<long>* bad = nullptr;
+    ~LateReader() {
+        if (p && mi_host_declared_kind(p, 64) != 2) (*bad)++;
+    }
+};
+thread_local LateReader t_late;
 
 int main(int argc, char** argv) {
     const double seconds = argc > 1 ? atof(argv[1]) : 1.0;
@@ -56,7 +71,11 @@ int main(int argc, char** argv) {
     while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < seconds) {
         std::vector<std::thread> shortlived;  // take a reader slot, read, exit: the slot comes back
         for (int r = 0; r < 8; r++)
-            shortlived.emplace_back([&] {
+            shortlived.emplace_back([&, r] {
+                if (r % 2) {  // a read at thread exit too, after the slot went back
+                    t_late.bad = &bad;
+                    t_late.p = held.data() + 256;
+                }
                 if (mi_host_declared_kind(held.data() + 128, 64) != 2) bad++;
             });
         for (auto& t : shortlived) t.join();

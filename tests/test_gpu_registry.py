@@ -179,3 +179,80 @@ def test_host_schedule_concurrent_workers_mixed_sizes():
     for t in ts:
         t.join()
     assert errors == []
+
+
+PAGE = 4096
+
+
+def _page_aligned(nbytes):
+    raw = np.zeros(nbytes + PAGE, np.uint8)
+    off = (-raw.ctypes.data) % PAGE
+    return raw, raw[off:off + nbytes]
+
+
+def test_pinned_ends_with_a_pageable_middle_are_not_zero_copy(gpu_dispatch):
+    """a range whose first and last pages are pinned (two
+    separate registrations) but whose middle is pageable must not be recorded
+    as pinned -- the zero-copy kernel would read unmapped pages.  It is either
+    refused (the ends' mappings differ) or recorded pageable and staged; a
+    reduce over it then gives the oracle's bits."""
+    m = _lib.mi()
+    raw, buf = _page_aligned(8 * PAGE)
+    p = buf.ctypes.data
+    assert m.mi_host_register(p, PAGE) == 0
+    assert m.mi_host_register(p + 7 * PAGE, PAGE) == 0
+    try:
+        rc = m.mi_host_declare(p, 8 * PAGE)
+        if rc == 0:
+            try:
+                assert m.mi_host_declared_kind(p, 8 * PAGE) == 2
+                n = 8 * PAGE // 8  # two fp32 operands of 4 pages each, both in the range
+                a = buf[:4 * PAGE].view(np.float32)
+                b = buf[4 * PAGE:].view(np.float32)
+                a[:] = rand_array(FP32, n, seed=5, specials=False)
+                b[:] = rand_array(FP32, n, seed=6, specials=False)
+                exp = b.copy()
+                oracle.comp_reduce(a.copy(), exp, FP32, 0, *_impls())
+                comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype(FP32), comp.reduction.sum)
+                assert_same(b, exp, FP32)
+            finally:
+                assert m.mi_host_undeclare(p) == 0
+        else:
+            assert rc == MI_E_INVALID and b"mappings" in m.mi_last_error()
+        # a declaration inside one registration stays pinned (zero-copy)
+        assert m.mi_host_declare(p + 7 * PAGE, PAGE) == 0
+        assert m.mi_host_declared_kind(p + 7 * PAGE, PAGE) == 1
+        assert m.mi_host_undeclare(p + 7 * PAGE) == 0
+    finally:
+        assert m.mi_host_unregister(p) == 0
+        assert m.mi_host_unregister(p + 7 * PAGE) == 0
+    del raw
+
+
+@pytest.mark.parametrize("n", [4099, (40 << 20) // 4 + 33])
+def test_unregistering_a_declared_pinned_buffer_demotes_it(gpu_dispatch, n):
+    """mi_host_unregister turns the declared ranges over
+    the buffer pageable before unpinning it, so a later reduce on the (still
+    valid, now pageable) memory is staged instead of read in place."""
+    m = _lib.mi()
+    raw_a, a8 = _page_aligned(n * 4)
+    raw_b, b8 = _page_aligned(n * 4)
+    a, b = a8.view(np.float32), b8.view(np.float32)
+    a[:] = rand_array(FP32, n, seed=11, specials=False)
+    b[:] = rand_array(FP32, n, seed=12, specials=False)
+    exp = b.copy()
+    oracle.comp_reduce_mt(a.copy(), exp, FP32, 0, 8, *_impls())
+    for x in (a, b):
+        assert m.mi_host_register(x.ctypes.data, x.nbytes) == 0
+        assert m.mi_host_declare(x.ctypes.data, x.nbytes) == 0
+        assert m.mi_host_declared_kind(x.ctypes.data, x.nbytes) == 1
+    for x in (a, b):
+        assert m.mi_host_unregister(x.ctypes.data) == 0
+        assert m.mi_host_declared_kind(x.ctypes.data, x.nbytes) == 2
+    try:
+        comp.comp_reduce(a.ctypes.data, n, b.ctypes.data, comp.datatype(FP32), comp.reduction.sum)
+    finally:
+        for x in (a, b):
+            assert m.mi_host_undeclare(x.ctypes.data) == 0
+    assert_same(b, exp, FP32)
+    del raw_a, raw_b

@@ -11,7 +11,15 @@
 //                     loads alive; nothing is written unless the XOR hits a
 //                     magic value);
 //   mic_write_stream  writes one stream of `bytes` (16-byte stores of a
-//                     constant).
+//                     constant);
+//   mic_mixed_streams reads the K streams and writes one stream in the same
+//                     launch, at the reduce's K:1 ratio, with no arithmetic:
+//                     each lane loads its vector of every input, keeps the
+//                     loads alive with an empty asm that takes them as
+//                     operands, and stores input 0's vector to the output
+//                     (the reads and the write interleaved
+//                     as the reduce interleaves them, which the separate
+//                     probes cannot show).
 // Each in the instruction flavours the library's kernels use (`flavor`):
 // 0 = global_load/store ... nt; 1 = buffer_load/store ... nt through a
 // per-workgroup descriptor; 2 (stores) = buffer_store ... sc1 nt, which the
@@ -94,6 +102,69 @@ __global__ void write_stream(u32x4* out, uint64_t nvec) {
     __builtin_nontemporal_store(one, out + v);
 }
 
+// The reduce's memory traffic without its arithmetic: K loads, one store
+// per lane, a tile of one vector per lane per block (the library's one-wave
+// tiles at block 64).  STORE_AUX 0 = global nt store; otherwise buffer_store
+// with those aux bits (kAuxNT: the fan-in's nt store, kAuxSC1NT: the 2-input
+// kernel's sc1 nt).  Loads: global nt (STORE_AUX 0) or buffer nt, as the
+// library's kernels pair them.
+struct MixArgs {
+    const u32x4* in[kMaxK];
+    u32x4* out;
+    uint64_t nvec;
+};
+
+template <int K, int STORE_AUX>
+__global__ void mixed_streams(MixArgs a) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    if ((uint64_t)blockIdx.x * blockDim.x >= a.nvec) return;
+    u32x4 x[K];
+    if constexpr (STORE_AUX == 0) {
+        const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (v >= a.nvec) return;
+#pragma unroll
+        for (int j = 0; j < K; j++) x[j] = __builtin_nontemporal_load(a.in[j] + v);
+#pragma unroll
+        for (int j = 1; j < K; j++) asm volatile("" ::"v"(x[j]));
+        __builtin_nontemporal_store(x[0], a.out + v);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            x[j] = __builtin_amdgcn_raw_buffer_load_b128(block_rsrc(a.in[j], a.nvec), threadIdx.x * 16u, 0, kAuxNT);
+#pragma unroll
+        for (int j = 1; j < K; j++) asm volatile("" ::"v"(x[j]));
+        __builtin_amdgcn_raw_buffer_store_b128(x[0], block_rsrc(a.out, a.nvec), threadIdx.x * 16u, 0, STORE_AUX);
+    }
+}
+
+typedef hipError_t (*MixFn)(dim3, dim3, unsigned, hipStream_t, const MixArgs&);
+
+template <int K, int AUX>
+hipError_t launch_mix(dim3 g, dim3 b, unsigned lds, hipStream_t s, const MixArgs& a) {
+    hipLaunchKernelGGL((mixed_streams<K, AUX>), g, b, lds, s, a);
+    return hipGetLastError();
+}
+
+template <int AUX>
+MixFn pick_mix_k(int k) {
+    switch (k) {
+        case 2: return launch_mix<2, AUX>;
+        case 3: return launch_mix<3, AUX>;
+        case 4: return launch_mix<4, AUX>;
+        case 6: return launch_mix<6, AUX>;
+        case 8: return launch_mix<8, AUX>;
+        case 12: return launch_mix<12, AUX>;
+        case 16: return launch_mix<16, AUX>;
+        default: return nullptr;
+    }
+}
+
+MixFn pick_mix(int k, int flavor) {
+    return flavor == 0 ? pick_mix_k<0>(k) : flavor == 1 ? pick_mix_k<kAuxNT>(k)
+                                                        : flavor == 2 ? pick_mix_k<kAuxSC1NT>(k) : nullptr;
+}
+
 template <int K, bool BUF>
 hipError_t launch_read(dim3 g, dim3 b, unsigned lds, hipStream_t s, const ReadArgs& a) {
     if (BUF)
@@ -173,6 +244,25 @@ __attribute__((visibility("default"))) int mic_write_stream(void* ptr, size_t by
     else
         hipLaunchKernelGGL(write_stream_buf<kAuxSC1NT>, g, b, lds, s, out, nvec);
     return (int)hipGetLastError();
+}
+
+// K read streams and one write stream in one launch (see mixed_streams):
+// `flavor` 0 = global nt loads + nt stores, 1 = buffer nt loads + nt stores
+// (the fan-in's), 2 = buffer nt loads + sc1 nt stores (the 2-input kernel's).
+// `out` may be ptrs[0] (in place, as ccl_comp_reduce).  0, the hipError_t,
+// or -1 on bad arguments.
+__attribute__((visibility("default"))) int mic_mixed_streams(const void* const* ptrs, int k, void* out, size_t bytes,
+                                                             int block, int waves_per_cu, int flavor, void* stream) {
+    MixFn fn = pick_mix(k, flavor);
+    if (!fn || !ptrs || !out || bytes % 16 || block < 64 || block > 1024) return -1;
+    MixArgs a{};
+    for (int j = 0; j < k; j++) a.in[j] = static_cast<const u32x4*>(ptrs[j]);
+    a.out = static_cast<u32x4*>(out);
+    a.nvec = bytes / 16;
+    const uint64_t blocks = (a.nvec + (uint64_t)block - 1) / (uint64_t)block;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
+    return (int)fn(dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
+                   static_cast<hipStream_t>(stream), a);
 }
 
 }  // extern "C"
