@@ -31,6 +31,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 GiB = 1 << 30
+T0 = time.perf_counter()  # process start (for wall_s_rank0)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 # name -> (description, ccl dtype id, element size, op, n_inputs, bucket bytes, flags)
@@ -127,60 +128,210 @@ def alloc_inputs(k, n, tdt, layout, device="cuda"):
     return [slab[j * stride:j * stride + n] for j in range(k)]
 
 
+TMPBUF_NOTE = ("oneCCL's nreduce layout (allreduce.cpp:326-394): reduce_buf is its own allocation, the k - 1 peer "
+               "chunks sit in consecutive slots of one tmp allocation")
+
+
+def alloc_tmpbuf(k, n, tdt, device="cuda"):
+    """The nreduce fan-in's operands as oneCCL lays them out: the schedule's
+    reduce_buf apart, and the k - 1 peer chunks received into consecutive
+    slots of one tmp buffer (src/coll/algorithms/allreduce/allreduce.cpp:
+    326-394), folded into reduce_buf in place."""
+    import torch
+    tmp = torch.empty((k - 1) * n, dtype=tdt, device=device)
+    return [torch.empty(n, dtype=tdt, device=device)] + [tmp[j * n:(j + 1) * n] for j in range(k - 1)]
+
+
 def torch_dtype(dt):
     import torch
     return {9: torch.float32, 11: torch.bfloat16, 8: torch.float16, 4: torch.int32, 6: torch.int64}[dt]
 
 
-def cpu_baseline(cfg, seconds):
-    """The oracle (CPU restatement of src/comp) timed on this host, bounded
-    sample: whole-bucket reduces repeated until ~`seconds` of CPU work."""
+def _cpulist(text):
+    """Linux cpulist syntax ("0-3,8,10-11") -> [int]."""
+    out = []
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out += range(int(a), int(b) + 1)
+        elif part:
+            out.append(int(part))
+    return out
+
+
+def core_plan():
+    """(NUMA node, one CPU per physical core of that node within this
+    process's affinity, CPUs in the affinity, cgroup CPU quota or None): the
+    node holding most allowed CPUs; of each core's hyperthread siblings the
+    first.  oneCCL pins one worker per core the same way
+    (src/exec/thread/worker.cpp:310-379, CCL_WORKER_AFFINITY)."""
+    aff = set(os.sched_getaffinity(0))
+    nodes = {}
+    for d in sorted(Path("/sys/devices/system/node").glob("node[0-9]*")):
+        try:
+            nodes[int(d.name[4:])] = set(_cpulist((d / "cpulist").read_text()))
+        except (OSError, ValueError):
+            continue
+    if not nodes:
+        nodes = {0: set(aff)}
+    node = max(nodes, key=lambda x: (len(nodes[x] & aff), -x))
+    seen, cores = set(), []
+    for c in sorted(nodes[node] & aff):
+        try:
+            sib = tuple(_cpulist(Path(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read_text()))
+        except (OSError, ValueError):
+            sib = (c,)
+        if sib not in seen:
+            seen.add(sib)
+            cores.append(c)
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return node, cores, len(aff), quota
+
+
+class PinnedPool:
+    """T threads, thread i pinned to cpus[i] for its whole life; run(job)
+    releases all of them on job(i) and returns when every one is done."""
+
+    def __init__(self, cpus):
+        import threading
+        self.n = len(cpus)
+        self.go = threading.Barrier(self.n + 1)
+        self.done = threading.Barrier(self.n + 1)
+        self.job = None
+        self.errors = []
+
+        def body(i, cpu):
+            try:
+                os.sched_setaffinity(0, {cpu})  # pid 0: the calling thread
+            except OSError as e:
+                self.errors.append(f"pin cpu {cpu}: {e}")
+            while True:
+                self.go.wait()
+                job = self.job
+                if job is None:
+                    return
+                try:
+                    job(i)
+                except Exception as e:  # noqa: BLE001
+                    self.errors.append(repr(e))
+                self.done.wait()
+
+        self.threads = [threading.Thread(target=body, args=(i, c), daemon=True) for i, c in enumerate(cpus)]
+        for t in self.threads:
+            t.start()
+
+    def run(self, job):
+        self.job = job
+        self.go.wait()
+        self.done.wait()
+        if self.errors:
+            raise RuntimeError("; ".join(self.errors[:3]))
+
+    def close(self):
+        self.job = None
+        self.go.wait()
+        for t in self.threads:
+            t.join()
+
+
+def cpu_sweep_point(cfg, cpus, seconds, use_ref):
+    """One thread count of the CPU baseline: len(cpus) threads, each pinned
+    to its core, each first-touching its own element range of every buffer
+    (so its pages sit on its own NUMA node), then reducing
+    that range with the reference's loop: k - 1 chained 2-input calls, as
+    CCL_WORKER_COUNT workers would each reduce their chunk.  Whole-bucket
+    reps repeated for ~`seconds`; returns (best GiB/s, median GiB/s, reps)."""
+    import ctypes
+
     import numpy as np
     import oracle
     desc, dt, es, op, k, bucket, flags = cfg
     n = bucket // es
-    rng = np.random.default_rng(0xC0FFEE)
+    T = len(cpus)
+    per = (n + T - 1) // T
+    per += (-per) % 64  # 256-byte aligned ranges: no two threads share a cache line
+    parts = [(min(n, i * per), min(n, (i + 1) * per)) for i in range(T)]
     npdt = oracle.NP_DTYPE[dt]
-    if dt in (9,):
-        ins = [rng.random(n, dtype=np.float32) * 2 - 1 for _ in range(k)]
-    elif dt in (4, 6):
-        ins = [rng.integers(-1000, 1000, n).astype(npdt) for _ in range(k)]
+    ins = [np.empty(n, npdt) for _ in range(k - 1)]  # untouched pages until each thread's fill
+    acc = np.empty(n, npdt)
+    if dt == 11:
+        vin, vacc = np.uint16(0x3E80), np.uint16(0x3F80)  # bf16 0.25, 1.0
+    elif dt == 8:
+        vin, vacc = np.uint16(0x3400), np.uint16(0x3C00)  # fp16 0.25, 1.0
+    elif dt in (9, 10):
+        vin, vacc = npdt(1.0 if op == 1 else 0.25), npdt(1.0)
     else:
-        f = rng.random(n, dtype=np.float32) * 2 - 1
-        ins = [oracle.f32_to_bf16(f, True) if dt == 11 else oracle.f32_to_fp16(f) for _ in range(k)]
-    acc = ins[0].copy()
+        vin, vacc = npdt(1 if op == 1 else 3), npdt(1)
+
+    def touch(i):
+        lo, hi = parts[i]
+        for x in ins:
+            x[lo:hi] = vin
+        acc[lo:hi] = vacc
+
+    if use_ref:
+        L = oracle.ref_comp_lib()
+        f = L.ref_ccl_comp_reduce_regular
+        ptrs = [x.ctypes.data for x in ins]
+        pacc = acc.ctypes.data
+
+        def reduce(i):
+            lo, hi = parts[i]
+            if hi > lo:
+                for p in ptrs:
+                    f(p + lo * es, hi - lo, pacc + lo * es, None, dt, es, op)
+    else:
+        def reduce(i):
+            lo, hi = parts[i]
+            if hi > lo:
+                for x in ins:
+                    oracle.comp_reduce(x[lo:hi], acc[lo:hi], dt, op)
+
+    pool = PinnedPool(cpus)
+    try:
+        pool.run(touch)
+        pool.run(reduce)  # warm
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 5 or (time.perf_counter() - t_start < seconds and len(times) < 400):
+            t0 = time.perf_counter()
+            pool.run(reduce)
+            times.append(time.perf_counter() - t0)
+    finally:
+        pool.close()
+    del ins, acc
+    return bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times)
+
+
+def cpu_baseline(cfg, seconds):
+    """The reference's own CPU reduce (or, for the bf16/fp16 types it cannot
+    reach standalone, the oracle's restatement) timed on this host's cores,
+    a bounded sample: 1 thread (one ccl_worker, CCL_WORKER_COUNT=1 default)
+    and a sweep of 8/16/32/64 pinned threads, each thread first-touching and
+    reducing its own range of the same bucket (cpu_sweep_point)."""
+    import numpy as np
+    import oracle
+    desc, dt, es, op, k, bucket, flags = cfg
     # the reference's own compiled CCL_REDUCE (oracle/_ref, its Release flags)
     # when it was built and the type is one it reaches; else the restatement
     use_ref = oracle.ref_comp_available() and dt not in (8, 11)
-    from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(16)
-
-    def one(nthreads):
-        t0 = time.perf_counter()
-        for x in ins[1:]:  # chained 2-input calls, as the reference
-            if use_ref:
-                oracle.ref_comp_reduce(x, acc, dt, op, nthreads, pool)
-            else:
-                oracle.comp_reduce_mt(x, acc, dt, op, nthreads)
-        return time.perf_counter() - t0
-
+    node, cores, n_aff, quota = core_plan()
+    limit = len(cores) if quota is None else min(len(cores), int(quota))
+    counts = [t for t in (1, 8, 16, 32, 64) if t <= max(1, limit)]
+    skipped = [t for t in (8, 16, 32, 64) if t not in counts]
+    share = max(seconds / (len(counts) + 1), 1.0)
     res = {}
-    for nthreads in (1, min(16, os.cpu_count() or 1)):
-        one(nthreads)  # first touch / warm
-        times = []
-        t_start = time.perf_counter()
-        while len(times) < 3 or (time.perf_counter() - t_start < seconds / 2 and len(times) < 200):
-            times.append(one(nthreads))
-        res[nthreads] = (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times))
-    pool.shutdown()
+    for t in counts:
+        res[t] = cpu_sweep_point(cfg, cores[:t] if cores else [0], share * (2 if t == 1 else 1), use_ref)
     port_1 = None
     if use_ref:  # the restatement on the same bucket, one thread, for comparison
-        tp = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            oracle.comp_reduce_mt(ins[1], acc, dt, op, 1)
-            tp.append(time.perf_counter() - t0)
-        port_1 = round(bucket / GiB / min(tp) * (k - 1), 3)
+        port_1 = round(cpu_sweep_point(cfg, cores[:1] if cores else [0], 1.0, False)[0], 3)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -190,8 +341,6 @@ def cpu_baseline(cfg, seconds):
     except OSError:
         pass
     (b1, m1, r1) = res[1]
-    nt = max(res)
-    (bn, mn, rn) = res[nt]
     # sanity probe, independent of the oracle: one core's memcpy bandwidth
     # over the same footprint (numpy's copy is a single-threaded memcpy)
     src = np.ones(bucket // 8, np.float64)
@@ -204,6 +353,10 @@ def cpu_baseline(cfg, seconds):
         ct.append(time.perf_counter() - t0)
     copy_gbps = 2 * src.nbytes / min(ct) / 1e9
     del src, dst
+    sweep = [{"threads": t, "best": round(b, 3), "median": round(m, 3), "reps": r,
+              "spread": round((b - m) / b, 4)} for t, (b, m, r) in sorted(res.items())]
+    head = 16 if 16 in res else max(res)
+    bn, mn, rn = res[head]
     return {
         "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "reference" if use_ref else "port",
         "traffic_GBps_1core": round(b1 * GiB * (k + 1) / 1e9, 1),
@@ -215,13 +368,21 @@ def cpu_baseline(cfg, seconds):
                     "Release flags, g++ -O3, oracle/_ref/libref_ccl_comp.so)") if use_ref else
                    "oracle/comp_oracle.c (CPU restatement of src/comp CCL_REDUCE loop, gcc -O3)") +
                   f" on the same {bucket // (1 << 20)} MiB bucket x {k}-input, best of {r1} reps (median {m1:.2f} "
-                  f"GiB/s); 1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default)",
+                  f"GiB/s); 1 thread = one ccl_worker (CCL_WORKER_COUNT=1 default), pinned to cpu "
+                  f"{cores[0] if cores else 0}, its own first touch",
         "port_1thread": port_1,
         "port_note": "port_1thread = oracle/comp_oracle.c on one thread, the restatement the parity tests use "
                      "(it states the x86 NaN rule explicitly: a checker, not the baseline)"
         if port_1 is not None else None,
-        "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": nt, "reps": rn,
-                         "note": "range split over threads, emulating CCL_WORKER_COUNT"},
+        "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": head, "reps": rn,
+                         "spread": round((bn - mn) / bn, 4), "sweep": sweep,
+                         "numa_node": node, "physical_cores_in_node": len(cores), "cpus_in_affinity": n_aff,
+                         "cgroup_cpu_quota": quota, "skipped_thread_counts": skipped,
+                         "cpus_used": cores[:max(res)],
+                         "note": "range split over threads, emulating CCL_WORKER_COUNT; one thread per physical core "
+                                 f"of NUMA node {node} (first hyperthread sibling), pinned; each thread first-touches "
+                                 "its own range of every buffer, then reduces it; thread counts above the node's "
+                                 "physical cores (or the cgroup's CPU quota) are skipped"},
         "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
     }
 
@@ -239,6 +400,43 @@ def plan(n_total, es, rank, world, scaling):
     lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
     _lib.check(_lib.mi().mi_shard_range(n_total, rank, world, 256, ctypes.byref(lo), ctypes.byref(hi)))
     return hi.value - lo.value, lo.value, n_total * es
+
+
+def input_bytes(k, n, es, layout):
+    """Device bytes alloc_inputs (or alloc_tmpbuf) takes for k inputs of n."""
+    if layout == "padded" and k == 2:
+        return pair_stride_bytes(n * es) + n * es
+    return k * n * es
+
+
+def memory_plan(config, layout, world, rank, scaling="weak"):
+    """Device bytes this rank allocates in each phase of `bench.py --gpus
+    world`, computed without a GPU (the N = 8 path's
+    allocations checked before a node runs it).  Phases: the headline bucket
+    (kept through the strong C2 split, which reuses it), its parity check's
+    temporaries (the torch fold: the expected result and one step's
+    intermediate), and, at N > 1 for c2, the strong C4 fan-in shard
+    (allocated after the headline bucket is freed).  Returns a dict with the
+    peak."""
+    desc, dt, es, op, k, bucket, flags = CONFIGS[config]
+    n_total = bucket // es
+    n, _, _ = plan(n_total, es, rank, world, scaling)
+    lay = "tmpbuf" if config == "c4-tmpbuf" else layout
+    head = input_bytes(k, n, es, lay)
+    lp = dt in (8, 11)
+    parity = n * (4 if lp else es) * 2  # exp + one step's temporary (fp32 for bf16/fp16)
+    out = {"config": config, "layout": lay, "world": world, "rank": rank, "elements": n,
+           "headline_inputs_bytes": head, "parity_temporaries_bytes": parity}
+    peak = head + parity
+    if world > 1 and config == "c2":
+        n2, _, _ = plan(n_total, es, rank, world, "strong")
+        n4, _, _ = plan(GiB // 4, 4, rank, world, "strong")
+        out["strong_c2_shard_elements"] = n2  # reuses the headline buffers
+        out["strong_c4_inputs_bytes"] = input_bytes(8, n4, 4, layout)
+        out["strong_c4_shard_elements"] = n4
+        peak = max(peak, out["strong_c4_inputs_bytes"])
+    out["peak_bytes"] = peak
+    return out
 
 
 def expected_result(ins, k, dt, op, flags):
@@ -374,6 +572,10 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     L.mic_write_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
+    has_mixed = hasattr(L, "mic_mixed_streams")
+    if has_mixed:
+        L.mic_mixed_streams.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     from oneccl_amd import _lib
     waves = ctypes.c_int(0)
     _lib.check(_lib.mi().mi_get_residency(-1, k, ctypes.byref(waves), None), "mi_get_residency")
@@ -402,17 +604,32 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
 
     r = best(lambda b, w, fl: L.mic_read_streams(arr, k, nb, b, w, fl, sink.data_ptr(), sh), (0, 1))
     wr = best(lambda b, w, fl: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, fl, sh), (0, 1, 2))
+    # the reads and the write in one launch, in place on ins[0] as the reduce
+    # runs (stores ins[0]'s own vectors back: no arithmetic)
+    mx = best(lambda b, w, fl: L.mic_mixed_streams(arr, k, ins[0].data_ptr(), nb, b, w, fl, sh),
+              (0, 1, 2)) if has_mixed else None
     if not r or not wr:
         return None
     t = (r[0] + wr[0]) / 1e3
     flav = {0: "global nt", 1: "buffer nt", 2: "buffer sc1 nt"}
-    return {"ceiling_TBps": round((k + 1) * nb / t / 1e12, 3),
-            "read_TBps": round(k * nb / (r[0] / 1e3) / 1e12, 3), "read_shape": [r[1], r[2], flav[r[3]]],
-            "write_TBps": round(nb / (wr[0] / 1e3) / 1e12, 3), "write_shape": [wr[1], wr[2], flav[wr[3]]],
-            "method": f"memory-only probes on this leg's buffers (tools/ceiling_probe.hip): {k} read streams and one "
-                      "write stream, each timed alone over block x wave-cap shapes and the load/store flavours the "
-                      "kernels use [block, waves/CU (0 = no cap), flavour], best taken; ceiling = (k+1) x bytes / "
-                      "(t_read + t_write)"}
+    mflav = {0: "global nt loads + nt stores", 1: "buffer nt loads + nt stores",
+             2: "buffer nt loads + sc1 nt stores"}
+    out = {"ceiling_TBps": round((k + 1) * nb / t / 1e12, 3),
+           "read_TBps": round(k * nb / (r[0] / 1e3) / 1e12, 3), "read_shape": [r[1], r[2], flav[r[3]]],
+           "write_TBps": round(nb / (wr[0] / 1e3) / 1e12, 3), "write_shape": [wr[1], wr[2], flav[wr[3]]],
+           "method": f"memory-only probes on this leg's buffers (tools/ceiling_probe.hip): {k} read streams and one "
+                     "write stream, each timed alone over block x wave-cap shapes and the load/store flavours the "
+                     "kernels use [block, waves/CU (0 = no cap), flavour], best taken; ceiling = (k+1) x bytes / "
+                     "(t_read + t_write)"}
+    if mx:
+        out["mixed_TBps"] = round((k + 1) * nb / (mx[0] / 1e3) / 1e12, 3)
+        out["mixed_shape"] = [mx[1], mx[2], mflav[mx[3]]]
+        out["mixed_ms"] = round(mx[0], 5)
+        out["mixed_method"] = (f"{k} read streams and the write stream in ONE launch (mic_mixed_streams): each lane "
+                               f"loads its 16-byte vector of all {k} inputs and stores input 0's back in place, no "
+                               "arithmetic; the reduce's own access pattern and K:1 read:write interleave, best over "
+                               "the same shapes and flavours")
+    return out
 
 
 def strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, steps, warmup, coll_dev, ins=None,
@@ -467,12 +684,16 @@ def config_legs(m, stream, layout, launches=10):
     legs = {}
     sh = stream.cuda_stream
     c2_other = {f"c2-layout-{x}": x for x in LAYOUTS if x != layout}  # the headline in the other layouts
-    for name in ("c3-bf16", "c3-fp16", "c4", "c4-bf16acc", "c5-int32-max", "c5-int64-prod", *c2_other):
+    for name in ("c3-bf16", "c3-fp16", "c4", "c4-tmpbuf", "c4-bf16acc", "c5-int32-max", "c5-int64-prod",
+                 *c2_other):
         desc, dt, es, op, k, bucket, flags = CONFIGS["c2" if name in c2_other else name]
         n = bucket // es
         if name in c2_other:
             desc = f"the headline (2-input fp32 sum, 1 GiB bucket), layout: {LAYOUT_NOTE[c2_other[name]]}"
-        ins = alloc_inputs(k, n, torch_dtype(dt), c2_other.get(name, layout))
+        if name == "c4-tmpbuf":
+            ins = alloc_tmpbuf(k, n, torch_dtype(dt))
+        else:
+            ins = alloc_inputs(k, n, torch_dtype(dt), c2_other.get(name, layout))
         for j, t in enumerate(ins):
             fill(t, 0xC0 + 131 * j)
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
@@ -496,13 +717,17 @@ def config_legs(m, stream, layout, launches=10):
         ceil = measured_ceiling(ins, k, n * es, stream)
         par = full_parity(lambda: _lib.check(step(), name), ins, k, dt, op, flags, 0xE0, "mi_reduce" if k == 2 else
                           "mi_reduce_multi")
-        legs[name] = {"workload": desc, "layout": LAYOUT_NOTE[c2_other.get(name, layout)],
+        legs[name] = {"workload": desc, "layout": TMPBUF_NOTE if name == "c4-tmpbuf" else
+                      LAYOUT_NOTE[c2_other.get(name, layout)],
                       "GiBps": round(bucket / GiB / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
                       "roofline_frac": round(algo / (ms / 1e3) / (HBM_PEAK_GBPS * 1e9), 4),
                       "parity": {"elements": par["elements"], "mismatches": par["mismatches"]}}
         if ceil:
             legs[name]["ceiling_TBps"] = ceil["ceiling_TBps"]
             legs[name]["frac_of_ceiling"] = round(algo / (ms / 1e3) / 1e12 / ceil["ceiling_TBps"], 4)
+            if "mixed_TBps" in ceil:
+                legs[name]["ceiling_mixed_TBps"] = ceil["mixed_TBps"]
+                legs[name]["frac_of_mixed_ceiling"] = round(algo / (ms / 1e3) / 1e12 / ceil["mixed_TBps"], 4)
             legs[name]["ceiling"] = ceil
         del ins, arr
         torch.cuda.empty_cache()
@@ -691,8 +916,7 @@ def main():
     m = _lib.mi()
     tdt = torch_dtype(dt)
     if args.config == "c4-tmpbuf":  # reduce_buf + one tmp buffer holding the k-1 peer chunks
-        tmp = torch.empty((k - 1) * n, dtype=tdt, device="cuda")
-        ins = [torch.empty(n, dtype=tdt, device="cuda")] + [tmp[j * n:(j + 1) * n] for j in range(k - 1)]
+        ins = alloc_tmpbuf(k, n, tdt)
     else:
         ins = alloc_inputs(k, n, tdt, args.layout)
     for j, t in enumerate(ins):
@@ -790,6 +1014,13 @@ def main():
         torch.cuda.empty_cache()
 
     traffic = pmc_traffic(args.config, traffic_per_launch)
+    mplan = memory_plan(args.config, args.layout, world, rank, args.scaling)
+    peak_dev = torch.cuda.max_memory_allocated()
+    if world > 1:
+        mem_max, = max_over_ranks([peak_dev], world, coll_dev)
+        mem_sum, = sum_over_ranks([peak_dev], world, coll_dev)
+    else:
+        mem_max = mem_sum = peak_dev
     if rank == 0:
         out = {
             "metric": "GiB/s device-resident fp32 sum-reduce of 1 GiB bucket; 1/2/4/8 MI355X"
@@ -809,8 +1040,7 @@ def main():
             "dtype": DTYPE_LABEL.get(dt, str(dt)),
             "data": "synthetic (uniform [-1,1) generated on device)",
             "config": {"workload": desc, "bucket_bytes_per_gpu": units_per_rank, "inputs": k,
-                       "layout": ("reduce_buf apart, the k - 1 peer chunks in one tmp allocation"
-                                  if args.config == "c4-tmpbuf" else LAYOUT_NOTE[args.layout]),
+                       "layout": TMPBUF_NOTE if args.config == "c4-tmpbuf" else LAYOUT_NOTE[args.layout],
                        "op": ["sum", "prod", "min", "max"][op], "dtype_id": dt, "flags": flags,
                        "parallelism": f"element-range shard x{world}, no collective",
                        "entry": "mi_reduce (include/mi_reduce.h) via ctypes, async on the torch stream"},
@@ -836,7 +1066,30 @@ def main():
         if ceil:
             out["roofline"]["ceiling_TBps"] = ceil["ceiling_TBps"]
             out["roofline"]["frac_of_ceiling"] = round(achieved / 1e3 / ceil["ceiling_TBps"], 4)
+            if "mixed_TBps" in ceil:
+                out["roofline"]["ceiling_mixed_TBps"] = ceil["mixed_TBps"]
+                out["roofline"]["frac_of_mixed_ceiling"] = round(achieved / 1e3 / ceil["mixed_TBps"], 4)
             out["roofline"]["ceiling"] = ceil
+        if legs and args.config == "c2":
+            # the same kernel and bucket where a caller's operands land: the
+            # headline's placement, separate allocations (what recv_reduce_entry
+            # hands over: the schedule's comm_buf and the user's buffer) and
+            # one allocation's consecutive slices; all in this run
+            pl = {args.layout: round(achieved / HBM_PEAK_GBPS, 4)}
+            for x in LAYOUTS:
+                if f"c2-layout-{x}" in legs:
+                    pl[x] = legs[f"c2-layout-{x}"]["roofline_frac"]
+            out["roofline"]["frac_by_placement"] = pl
+            out["roofline"]["placement_note"] = (
+                f"headline: {args.layout}; 'separate' (one allocation per operand) is the placement oneCCL's "
+                "recv_reduce_entry produces (comm_buf from the schedule's buffer, inout the user's), DESIGN.md §6")
+        out["memory"] = {"planned_peak_bytes_rank0": mplan["peak_bytes"],
+                         "torch_max_allocated_bytes_max_rank": int(mem_max),
+                         "torch_max_allocated_bytes_sum_ranks": int(mem_sum),
+                         "note": "planned = memory_plan() (bench.py, computed without a GPU); measured = "
+                                 "torch.cuda.max_memory_allocated() per rank (the config legs' buffers included at "
+                                 "N = 1)"}
+        out["wall_s_rank0"] = round(time.perf_counter() - T0, 2)
         if rehearsal:
             out["rehearsal"] = True
             out["rehearsal_note"] = (f"{pg_world} ranks on {n_devices} device(s): a rehearsal of the N-rank path, "

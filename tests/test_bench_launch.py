@@ -17,6 +17,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 import bench  # noqa: E402
+GIB = 1 << 30
 
 
 def test_rank_plan_env():
@@ -247,3 +248,65 @@ def test_alloc_inputs_layouts(layout, k, dtype):
     assert bench.pair_stride_bytes(bench.PAIR_OFFSET + 16) == bench.PAIR_OFFSET + 16 + bench.PAIR_GAP
     assert bench.pair_stride_bytes(1 << 30) == bench.PAIR_OFFSET
     assert layout in bench.LAYOUTS and layout in bench.LAYOUT_NOTE
+
+
+def test_alloc_tmpbuf_is_oneccl_nreduce_layout():
+    """c4-tmpbuf: reduce_buf its own allocation, the k - 1
+    peer chunks in consecutive slots of one tmp buffer (allreduce.cpp:326-394)."""
+    import torch
+    k, n = 8, 1000
+    ins = bench.alloc_tmpbuf(k, n, torch.float32, device="cpu")
+    assert len(ins) == k and all(t.numel() == n for t in ins)
+    tmp_base = ins[1].untyped_storage().data_ptr()
+    assert ins[0].untyped_storage().data_ptr() != tmp_base
+    for j in range(2, k):
+        assert ins[j].untyped_storage().data_ptr() == tmp_base
+        assert ins[j].data_ptr() - ins[j - 1].data_ptr() == n * 4
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_memory_plan_n8_without_a_gpu(world):
+    """the per-rank allocation plan of `bench.py --gpus N`
+    (padded pair, then at N > 1 the strong-split C2 shard reusing it and the
+    C4 fan-in shard) is computed on the CPU; the strong shards of all ranks
+    tile the bucket, and a rehearsal of 8 ranks on one 288 GB GPU fits."""
+    plans = [bench.memory_plan("c2", "padded", world, r) for r in range(world)]
+    for p in plans:
+        assert p["headline_inputs_bytes"] == bench.PAIR_OFFSET + GIB  # weak: a full 1 GiB bucket per rank
+        assert p["peak_bytes"] >= p["headline_inputs_bytes"]
+    if world > 1:
+        assert sum(p["strong_c2_shard_elements"] for p in plans) == GIB // 4
+        assert sum(p["strong_c4_shard_elements"] for p in plans) == GIB // 4
+        assert all(p["strong_c4_shard_elements"] % 256 == 0 for p in plans[:-1])
+        assert all(p["strong_c4_inputs_bytes"] == 8 * 4 * p["strong_c4_shard_elements"] for p in plans)
+    else:
+        assert "strong_c4_inputs_bytes" not in plans[0]
+    # every rank on one GPU (the rehearsal) stays well inside 288 GB
+    assert sum(p["peak_bytes"] for p in plans) < 0.5 * 288e9
+
+
+def test_memory_plan_layouts_and_tmpbuf():
+    assert bench.memory_plan("c2", "separate", 1, 0)["headline_inputs_bytes"] == 2 * GIB
+    assert bench.memory_plan("c2", "one", 1, 0)["headline_inputs_bytes"] == 2 * GIB
+    p = bench.memory_plan("c4-tmpbuf", "padded", 1, 0)
+    assert p["layout"] == "tmpbuf" and p["headline_inputs_bytes"] == 8 * GIB
+    p = bench.memory_plan("c3-bf16", "padded", 1, 0)
+    assert p["parity_temporaries_bytes"] == 2 * (128 << 20) * 4  # fp32 fold temporaries
+
+
+def test_core_plan_one_cpu_per_physical_core():
+    import os
+    node, cores, n_aff, quota = bench.core_plan()
+    assert cores and set(cores) <= set(os.sched_getaffinity(0))
+    assert len(cores) == len(set(cores)) and n_aff >= len(cores)
+    assert quota is None or quota > 0
+
+
+def test_cpu_sweep_point_pins_and_reduces():
+    """A small sample of the threaded baseline: 2 pinned threads, each first-
+    touching and reducing its own range; rates are positive and best >= median."""
+    import os
+    cfg = ("fp32 sum", 9, 4, 0, 2, 8 << 20, 0)
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    b, m, r = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
+    assert b >= m > 0 and r >= 5
