@@ -163,7 +163,7 @@ def core_plan():
     """(NUMA node, one CPU per physical core of that node within this
     process's affinity, CPUs in the affinity, cgroup CPU quota or None): the
     node holding most allowed CPUs; of each core's hyperthread siblings the
-    first.  oneCCL pins one worker per core the same way
+    first; ordered round robin over the node's L3 domains.  oneCCL pins one worker per core the same way
     (src/exec/thread/worker.cpp:310-379, CCL_WORKER_AFFINITY)."""
     aff = set(os.sched_getaffinity(0))
     nodes = {}
@@ -184,6 +184,18 @@ def core_plan():
         if sib not in seen:
             seen.add(sib)
             cores.append(c)
+    # round robin over the L3 domains (a Zen 5 CCD: 8 cores behind one link
+    # to the memory side), so T threads draw on min(T, domains) links: the
+    # first T cores of one CCD would measure that CCD's link, not the node
+    groups = {}
+    for c in cores:
+        try:
+            key = Path(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read_text().strip()
+        except OSError:
+            key = ""
+        groups.setdefault(key, []).append(c)
+    lists = list(groups.values())
+    cores = [lst[i] for i in range(max(map(len, lists), default=0)) for lst in lists if i < len(lst)]
     quota = None
     try:
         q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
@@ -380,7 +392,8 @@ def cpu_baseline(cfg, seconds):
                          "cgroup_cpu_quota": quota, "skipped_thread_counts": skipped,
                          "cpus_used": cores[:max(res)],
                          "note": "range split over threads, emulating CCL_WORKER_COUNT; one thread per physical core "
-                                 f"of NUMA node {node} (first hyperthread sibling), pinned; each thread first-touches "
+                                 f"of NUMA node {node} (first hyperthread sibling), taken round robin over the node's L3 "
+                                 "domains (CCDs), pinned; each thread first-touches "
                                  "its own range of every buffer, then reduces it; thread counts above the node's "
                                  "physical cores (or the cgroup's CPU quota) are skipped"},
         "cpu_model": cpu_model, "host_cpus": os.cpu_count(),

@@ -21,11 +21,20 @@
 //            host memory by the caller's word, nothing looked up
 //   bf16 / fp16        ccl_{bf16,fp16}_reduce with no word (every operand
 //            looked up): the user ops' call before that patch
+//   foldbf16 / foldfp16  mi_host_reduce alone (the drop-in's CPU fold,
+//            include/mi_host_reduce.h) with the avx512bf / fp16 flags: the
+//            fold without the entry point around it
+//   schedbf16 / schedfp16 / schedi16  ccl_comp_reduce of bf16 / fp16 /
+//            int16 under a schedule without a stream
 //   refbf16 / reffp16  the reference's own AVX-512 body (avx512bf /
 //            avx512f impl) from oracle/_ref/libref_comp.so: what the user
 //            op runs in the reference (bf16.cpp:98-109, fp16_intrisics.hpp:204)
 // Also prints the HIP pointer lookups the drop-in made per call.
+// SW_CPUS=c0,c1,...: thread t pins itself to c[t % n] before its buffers are
+// allocated (unset: unpinned).
 #include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -38,6 +47,8 @@
 #include <vector>
 
 #include "mi_ccl_comp.h"
+#include "mi_host_reduce.h"
+#include "mi_reduce.h"
 
 typedef int (*ref_reduce_t)(const void*, size_t, void*, size_t*, int, size_t, int);
 typedef int (*ref_lp_t)(int, int, const uint16_t*, uint16_t*, size_t);
@@ -52,7 +63,8 @@ int main(int argc, char** argv) {
     const std::string mode = argc > 3 ? argv[3] : "default";
     ref_reduce_t ref = nullptr;
     ref_lp_t ref_lp = nullptr;
-    const bool lp = mode.find("bf16") != std::string::npos || mode.find("fp16") != std::string::npos;
+    const bool lp = mode.find("bf16") != std::string::npos || mode.find("fp16") != std::string::npos ||
+                    mode.find("i16") != std::string::npos;
     const size_t es = lp ? 2 : sizeof(float);
     if (mode == "refbf16" || mode == "reffp16") {
         const char* path = getenv("REF_LP_SO") ? getenv("REF_LP_SO") : "oracle/_ref/libref_comp.so";
@@ -75,9 +87,22 @@ int main(int argc, char** argv) {
     const long iters = std::max<long>(2000, (long)(400000000.0 / (double)(n + 256)));
     std::vector<double> us(T);
     std::vector<double> lookups(T);
+    std::vector<int> pin;
+    if (const char* v = getenv("SW_CPUS"))
+        for (const char* c = v; *c;) {
+            pin.push_back(atoi(c));
+            while (*c && *c != ',') c++;
+            if (*c == ',') c++;
+        }
     std::vector<std::thread> th;
     for (int t = 0; t < T; t++)
         th.emplace_back([&, t] {
+            if (!pin.empty()) {
+                cpu_set_t cs;
+                CPU_ZERO(&cs);
+                CPU_SET(pin[t % pin.size()], &cs);
+                pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
+            }
             std::vector<float> a(n, 1.f), b(n, 1.f);
             // 2-byte modes: bf16 1.0 (0x3f80) / fp16 1.0 (0x3c00), n elements
             const uint16_t one = mode.find("bf16") != std::string::npos ? 0x3f80 : 0x3c00;
@@ -86,7 +111,8 @@ int main(int argc, char** argv) {
                 mi_ccl_comp_register_host_buffer(a.data(), n * sizeof(float));
                 mi_ccl_comp_register_host_buffer(b.data(), n * sizeof(float));
             }
-            if (mode == "sched") mi_ccl_comp_shim_sched(1);
+            if (mode.compare(0, 5, "sched") == 0) mi_ccl_comp_shim_sched(1);
+            const void* fins[2] = {b2.data(), a2.data()};
             const size_t nb = n * sizeof(float);
             auto call = [&] {
                 if (ref) ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0);
@@ -94,6 +120,23 @@ int main(int argc, char** argv) {
                 else if (mode == "mpibf16") mi_ccl_bf16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
                 else if (mode == "mpifp16") mi_ccl_fp16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
                 else if (mode == "bf16") mi_ccl_bf16_reduce(a2.data(), n, b2.data(), nullptr, 0);
+                else if (mode == "foldbf16")
+                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                else if (mode == "foldfp16") mi_host_reduce(fins, 2, b2.data(), n, MI_FLOAT16, 0, MI_F_MINMAX_INOUT_FIRST);
+                else if (mode == "schedbf16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 11, 0);
+                else if (mode == "schedfp16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 8, 0);
+                else if (mode == "schedi16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                // diagnostic pairs: does the bf16 fold slow the shim around it?
+                else if (mode == "schedi16+foldbf16") {
+                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                } else if (mode == "foldi16+foldbf16") {
+                    mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
+                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                } else if (mode == "schedi16x2") {
+                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                } else if (mode == "foldi16") mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
                 else if (mode == "fp16") mi_ccl_fp16_reduce(a2.data(), n, b2.data(), nullptr, 0);
                 else if (mode == "copy") mi_ccl_comp_copy(a.data(), b.data(), nb, 0);
                 else if (mode == "copyhost") mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0);
@@ -119,8 +162,8 @@ int main(int argc, char** argv) {
     const char* mi = getenv("MI_ROCTX");
     const char* itt = getenv("CCL_ITT_LEVEL");
     const bool roctx_on = mi ? strcmp(mi, "0") != 0 : (itt && atoi(itt) > 0);
-    printf("{\"mode\": \"%s%s\", \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
+    printf("{\"mode\": \"%s%s\", \"pinned\": %s, \"threads\": %d, \"elements\": %zu, \"bytes\": %zu, \"median_us\": %.3f, "
            "\"max_us\": %.3f, \"lookups_per_call\": %.2f, \"iters\": %ld}\n",
-           mode.c_str(), roctx_on ? " (roctx on)" : "", T, n, n * es, s[T / 2], s[T - 1], lk, iters);
+           mode.c_str(), roctx_on ? " (roctx on)" : "", pin.empty() ? "false" : "true", T, n, n * es, s[T / 2], s[T - 1], lk, iters);
     fflush(stdout);
 }
