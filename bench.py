@@ -422,25 +422,43 @@ def input_bytes(k, n, es, layout):
     return k * n * es
 
 
+def parity_bytes(n, dt, es):
+    """Device temporaries of full_parity's torch fold (expected_result): the
+    running accumulator, the next input and their result (in fp32 for
+    bf16/fp16, plus the rounded result), or the accumulator and its sum."""
+    return n * 4 * 3 + n * es if dt in (8, 11) else 2 * n * es
+
+
 def memory_plan(config, layout, world, rank, scaling="weak"):
     """Device bytes this rank allocates in each phase of `bench.py --gpus
     world`, computed without a GPU (the N = 8 path's
     allocations checked before a node runs it).  Phases: the headline bucket
     (kept through the strong C2 split, which reuses it), its parity check's
     temporaries (the torch fold: the expected result and one step's
-    intermediate), and, at N > 1 for c2, the strong C4 fan-in shard
-    (allocated after the headline bucket is freed).  Returns a dict with the
-    peak."""
+    intermediates), at N = 1 for c2 the config legs (each allocated and
+    freed in turn while the headline buffers are held), and at N > 1 for c2
+    the strong C4 fan-in shard (allocated after the headline bucket is
+    freed).  Returns a dict with the peak."""
     desc, dt, es, op, k, bucket, flags = CONFIGS[config]
     n_total = bucket // es
     n, _, _ = plan(n_total, es, rank, world, scaling)
     lay = "tmpbuf" if config == "c4-tmpbuf" else layout
     head = input_bytes(k, n, es, lay)
-    lp = dt in (8, 11)
-    parity = n * (4 if lp else es) * 2  # exp + one step's temporary (fp32 for bf16/fp16)
+    parity = parity_bytes(n, dt, es)
     out = {"config": config, "layout": lay, "world": world, "rank": rank, "elements": n,
            "headline_inputs_bytes": head, "parity_temporaries_bytes": parity}
     peak = head + parity
+    if world == 1 and config == "c2":
+        # the config legs run while the headline buffers are still held
+        legs = {}
+        for name in ("c3-bf16", "c3-fp16", "c4", "c4-tmpbuf", "c4-bf16acc", "c5-int32-max", "c5-int64-prod",
+                     "c2-layout-one", "c2-layout-separate"):
+            _, ldt, les, _, lk, lbucket, _ = CONFIGS["c2" if name.startswith("c2-") else name]
+            ln = lbucket // les
+            llay = "tmpbuf" if name == "c4-tmpbuf" else name[len("c2-layout-"):] if name.startswith("c2-") else layout
+            legs[name] = input_bytes(lk, ln, les, llay) + parity_bytes(ln, ldt, les)
+        out["config_legs_bytes"] = legs
+        peak = max(peak, head + max(legs.values()))
     if world > 1 and config == "c2":
         n2, _, _ = plan(n_total, es, rank, world, "strong")
         n4, _, _ = plan(GiB // 4, 4, rank, world, "strong")
