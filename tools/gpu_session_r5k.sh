@@ -32,3 +32,12 @@ for pc in c2 c4; do
         python3 "$GRAFT_REPO_ROOT/bench.py" --config $pc --steps 20 --warmup 5 --no-cpu-baseline --no-host-leg --no-config-legs \
         > "$GRAFT_REPO_ROOT/$O/prof_$pc.out" 2> "$GRAFT_REPO_ROOT/$O/prof_$pc.err") || exit $?
 done
+# 5. HBM bytes per launch of the C2 and C4 kernels: FETCH_SIZE and WRITE_SIZE
+#    in separate --pmc passes (MI355X_MICROARCH.md, HBM / rocprofv3)
+for pc in c2 c4; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d "$GRAFT_REPO_ROOT/$O/pmc_$pc/pmc_$ctr" -o bench -- \
+            python3 "$GRAFT_REPO_ROOT/bench.py" --config $pc --steps 5 --warmup 2 --no-cpu-baseline --no-host-leg --no-config-legs \
+            > "$GRAFT_REPO_ROOT/$O/pmc_${pc}_$ctr.out" 2> "$GRAFT_REPO_ROOT/$O/pmc_${pc}_$ctr.err") || exit $?
+    done
+done

@@ -113,6 +113,7 @@ int main(int argc, char** argv) {
             }
             if (mode.compare(0, 5, "sched") == 0) mi_ccl_comp_shim_sched(1);
             const void* fins[2] = {b2.data(), a2.data()};
+            const void* f32ins[2] = {b.data(), a.data()};
             const size_t nb = n * sizeof(float);
             auto call = [&] {
                 if (ref) ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0);
@@ -137,6 +138,7 @@ int main(int argc, char** argv) {
                     mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
                     mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
                 } else if (mode == "foldi16") mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
+                else if (mode == "foldf32") mi_host_reduce(f32ins, 2, b.data(), n, MI_FLOAT32, 0, 0);
                 else if (mode == "fp16") mi_ccl_fp16_reduce(a2.data(), n, b2.data(), nullptr, 0);
                 else if (mode == "copy") mi_ccl_comp_copy(a.data(), b.data(), nb, 0);
                 else if (mode == "copyhost") mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0);
