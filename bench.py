@@ -423,10 +423,11 @@ def input_bytes(k, n, es, layout):
 
 
 def parity_bytes(n, dt, es):
-    """Device temporaries of full_parity's torch fold (expected_result): the
-    running accumulator, the next input and their result (in fp32 for
-    bf16/fp16, plus the rounded result), or the accumulator and its sum."""
-    return n * 4 * 3 + n * es if dt in (8, 11) else 2 * n * es
+    """Device temporaries of full_parity: the torch fold (expected_result) --
+    the accumulator and its sum, and for bf16/fp16 the widened input and the
+    storage rounding's round trip in fp32 -- plus the mismatch mask (one byte
+    per element)."""
+    return (n * 4 * 4 + n * es if dt in (8, 11) else 2 * n * es) + n
 
 
 def memory_plan(config, layout, world, rank, scaling="weak"):
@@ -519,7 +520,9 @@ def count_mismatches(got, exp):
     """Elements whose bits differ (NaN payloads included)."""
     import torch
     ib = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[got.element_size()]
-    return int(torch.ne(got.view(ib), exp.view(ib)).sum().item())
+    # count_nonzero reads the bool mask as is (a .sum() of it made an int64
+    # copy: 8 bytes per element, 2 GiB for the headline bucket)
+    return int(torch.count_nonzero(torch.ne(got.view(ib), exp.view(ib))).item())
 
 
 def full_parity(run_once, ins, k, dt, op, flags, seed0, entry):

@@ -291,7 +291,7 @@ def test_memory_plan_layouts_and_tmpbuf():
     p = bench.memory_plan("c4-tmpbuf", "padded", 1, 0)
     assert p["layout"] == "tmpbuf" and p["headline_inputs_bytes"] == 8 * GIB
     p = bench.memory_plan("c3-bf16", "padded", 1, 0)
-    assert p["parity_temporaries_bytes"] == (128 << 20) * (3 * 4 + 2)  # fp32 fold temporaries + result
+    assert p["parity_temporaries_bytes"] == (128 << 20) * (4 * 4 + 2 + 1)  # fp32 fold temporaries, result, mask
 
 
 def test_core_plan_one_cpu_per_physical_core():

@@ -87,6 +87,28 @@ int main(int argc, char** argv) {
     const long iters = std::max<long>(2000, (long)(400000000.0 / (double)(n + 256)));
     std::vector<double> us(T);
     std::vector<double> lookups(T);
+    enum {
+        M_DEFAULT, M_REF, M_REFBF16, M_REFFP16, M_MPIBF16, M_MPIFP16, M_BF16, M_FP16, M_FOLDBF16, M_FOLDFP16,
+        M_FOLDI16, M_FOLDF32, M_SCHEDBF16, M_SCHEDFP16, M_SCHEDI16, M_SCHEDI16_FOLDBF16, M_FOLDI16_FOLDBF16,
+        M_SCHEDI16X2, M_COPY, M_COPYHOST, M_MEMCPY
+    };
+    const struct {
+        const char* name;
+        int id;
+    } modes[] = {{"default", M_DEFAULT}, {"reg", M_DEFAULT}, {"sched", M_DEFAULT}, {"ref", M_REF},
+                 {"refbf16", M_REFBF16}, {"reffp16", M_REFFP16}, {"mpibf16", M_MPIBF16}, {"mpifp16", M_MPIFP16},
+                 {"bf16", M_BF16}, {"fp16", M_FP16}, {"foldbf16", M_FOLDBF16}, {"foldfp16", M_FOLDFP16},
+                 {"foldi16", M_FOLDI16}, {"foldf32", M_FOLDF32}, {"schedbf16", M_SCHEDBF16},
+                 {"schedfp16", M_SCHEDFP16}, {"schedi16", M_SCHEDI16}, {"schedi16+foldbf16", M_SCHEDI16_FOLDBF16},
+                 {"foldi16+foldbf16", M_FOLDI16_FOLDBF16}, {"schedi16x2", M_SCHEDI16X2}, {"copy", M_COPY},
+                 {"copyhost", M_COPYHOST}, {"memcpy", M_MEMCPY}};
+    int mid = -1;
+    for (const auto& m : modes)
+        if (mode == m.name) mid = m.id;
+    if (mid < 0) {
+        fprintf(stderr, "unknown mode %s\n", mode.c_str());
+        return 2;
+    }
     std::vector<int> pin;
     if (const char* v = getenv("SW_CPUS"))
         for (const char* c = v; *c;) {
@@ -115,35 +137,44 @@ int main(int argc, char** argv) {
             const void* fins[2] = {b2.data(), a2.data()};
             const void* f32ins[2] = {b.data(), a.data()};
             const size_t nb = n * sizeof(float);
+            // the mode is resolved to an id once: a chain of string compares
+            // inside the timed loop cost tens of ns per call (round 5)
             auto call = [&] {
-                if (ref) ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0);
-                else if (ref_lp) ref_lp(mode == "refbf16" ? 2 : 3, 0, a2.data(), b2.data(), n);
-                else if (mode == "mpibf16") mi_ccl_bf16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
-                else if (mode == "mpifp16") mi_ccl_fp16_reduce_host(a2.data(), n, b2.data(), nullptr, 0);
-                else if (mode == "bf16") mi_ccl_bf16_reduce(a2.data(), n, b2.data(), nullptr, 0);
-                else if (mode == "foldbf16")
-                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
-                else if (mode == "foldfp16") mi_host_reduce(fins, 2, b2.data(), n, MI_FLOAT16, 0, MI_F_MINMAX_INOUT_FIRST);
-                else if (mode == "schedbf16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 11, 0);
-                else if (mode == "schedfp16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 8, 0);
-                else if (mode == "schedi16") mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
-                // diagnostic pairs: does the bf16 fold slow the shim around it?
-                else if (mode == "schedi16+foldbf16") {
-                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
-                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
-                } else if (mode == "foldi16+foldbf16") {
-                    mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
-                    mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
-                } else if (mode == "schedi16x2") {
-                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
-                    mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
-                } else if (mode == "foldi16") mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
-                else if (mode == "foldf32") mi_host_reduce(f32ins, 2, b.data(), n, MI_FLOAT32, 0, 0);
-                else if (mode == "fp16") mi_ccl_fp16_reduce(a2.data(), n, b2.data(), nullptr, 0);
-                else if (mode == "copy") mi_ccl_comp_copy(a.data(), b.data(), nb, 0);
-                else if (mode == "copyhost") mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0);
-                else if (mode == "memcpy") memcpy(b.data(), a.data(), nb);
-                else mi_ccl_comp_reduce(a.data(), n, b.data(), nullptr, 9, 0);
+                switch (mid) {
+                    case M_REF: ref(a.data(), n, b.data(), nullptr, 9, sizeof(float), 0); break;
+                    case M_REFBF16: ref_lp(2, 0, a2.data(), b2.data(), n); break;
+                    case M_REFFP16: ref_lp(3, 0, a2.data(), b2.data(), n); break;
+                    case M_MPIBF16: mi_ccl_bf16_reduce_host(a2.data(), n, b2.data(), nullptr, 0); break;
+                    case M_MPIFP16: mi_ccl_fp16_reduce_host(a2.data(), n, b2.data(), nullptr, 0); break;
+                    case M_BF16: mi_ccl_bf16_reduce(a2.data(), n, b2.data(), nullptr, 0); break;
+                    case M_FP16: mi_ccl_fp16_reduce(a2.data(), n, b2.data(), nullptr, 0); break;
+                    case M_FOLDBF16:
+                        mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                        break;
+                    case M_FOLDFP16: mi_host_reduce(fins, 2, b2.data(), n, MI_FLOAT16, 0, MI_F_MINMAX_INOUT_FIRST); break;
+                    case M_FOLDI16: mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0); break;
+                    case M_FOLDF32: mi_host_reduce(f32ins, 2, b.data(), n, MI_FLOAT32, 0, 0); break;
+                    case M_SCHEDBF16: mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 11, 0); break;
+                    case M_SCHEDFP16: mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 8, 0); break;
+                    case M_SCHEDI16: mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0); break;
+                    // diagnostic pairs: does the bf16 fold slow the entry point around it?
+                    case M_SCHEDI16_FOLDBF16:
+                        mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                        mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                        break;
+                    case M_FOLDI16_FOLDBF16:
+                        mi_host_reduce(fins, 2, b2.data(), n, MI_INT16, 0, 0);
+                        mi_host_reduce(fins, 2, b2.data(), n, MI_BFLOAT16, 0, MI_F_MINMAX_INOUT_FIRST | MI_F_BF16_RNE);
+                        break;
+                    case M_SCHEDI16X2:
+                        mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                        mi_ccl_comp_reduce(a2.data(), n, b2.data(), nullptr, 2, 0);
+                        break;
+                    case M_COPY: mi_ccl_comp_copy(a.data(), b.data(), nb, 0); break;
+                    case M_COPYHOST: mi_ccl_comp_copy_host(a.data(), b.data(), nb, 0); break;
+                    case M_MEMCPY: memcpy(b.data(), a.data(), nb); break;
+                    default: mi_ccl_comp_reduce(a.data(), n, b.data(), nullptr, 9, 0);  // default, reg, sched
+                }
             };
             for (long i = 0; i < std::min<long>(2000, iters); i++) call();
             const size_t l0 = mi_ccl_comp_pointer_lookups();
