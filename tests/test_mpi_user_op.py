@@ -149,3 +149,33 @@ def test_concurrent_user_ops_make_no_lookup(dt, entry):
     for w in ws:
         w.join()
     assert errors == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,entry", [(BF16, "mi_ccl_bf16_reduce_host"), (FP16, "mi_ccl_fp16_reduce_host")])
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+def test_large_user_op_bucket_on_the_gpu(dt, entry, kind):
+    """Above the dispatcher's threshold (16 MiB) a user op's bucket is split
+    between the calling thread and the GPU: its operands are looked up (their
+    kinds pick pinned zero-copy or staging), and the bits are the oracle's
+    under the impl type in force."""
+    import torch
+    s = _lib.shim()
+    b_impl, f_impl = comp.impl_types()
+    n = (40 << 20) // 2 + 77
+    a = rand_array(dt, n, seed=61, specials=False)
+    b0 = rand_array(dt, n, seed=62, specials=False)
+    exp = b0.copy()
+    oracle.comp_reduce_mt(a, exp, dt, 0, 8, int(b_impl), int(f_impl))
+    if kind == "pinned":
+        ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+        hb = torch.from_numpy(b0.view(np.uint8).copy()).pin_memory()
+        pa, pb = ha.data_ptr(), hb.data_ptr()
+    else:
+        b = b0.copy()
+        pa, pb = a.ctypes.data, b.ctypes.data
+    n0 = s.mi_ccl_comp_pointer_lookups()
+    _lib.check_shim(getattr(s, entry)(pa, n, pb, None, 0), entry)
+    assert s.mi_ccl_comp_pointer_lookups() - n0 > 0
+    got = hb.numpy().view(a.dtype) if kind == "pinned" else b
+    assert_same(got, exp, dt, f"{entry} {kind}")
