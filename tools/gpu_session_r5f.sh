@@ -1,4 +1,6 @@
 # round 5 session f: the 4 KiB bf16 call under a host schedule with the
+# (historical: the diagnostic shim builds under tools/diag_* that this session loaded were
+# one-off variants of comp.cpp and are not kept; results: profiles/round5_host/isolate_*)
 # product shim, a shim without the host-worker accounting (HostCall), and one
 # with 128-byte accounting slots (tools/diag_*: diagnostic builds only)
 set -u

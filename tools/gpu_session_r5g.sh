@@ -1,4 +1,6 @@
 # round 5 session g: TSC cycles inside the fold vs the whole call (diagnostic shim build)
+# (historical: the diagnostic shim builds under tools/diag_* that this session loaded were
+# one-off variants of comp.cpp and are not kept; results: profiles/round5_host/isolate_*)
 set -u
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r5g
