@@ -619,7 +619,7 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
     sh = stream.cuda_stream
     nb = nbytes - nbytes % 16
 
-    def best(launch, flavors):
+    def best(launch, flavors, shapes=shapes):
         res = []
         for fl in flavors:
             for block, w in shapes:
@@ -640,8 +640,11 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
     wr = best(lambda b, w, fl: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, fl, sh), (0, 1, 2))
     # the reads and the write in one launch, in place on ins[0] as the reduce
     # runs (stores ins[0]'s own vectors back: no arithmetic)
+    # every residency the LDS granules allow for one-wave blocks (the library
+    # picks one of them per k), so the ceiling is not the library's own choice
+    mixed_shapes = [(64, w) for w in sorted({waves.value, 5, 8, 9, 11, 16, 21, 25})] + shapes[1:]
     mx = best(lambda b, w, fl: L.mic_mixed_streams(arr, k, ins[0].data_ptr(), nb, b, w, fl, sh),
-              (0, 1, 2)) if has_mixed else None
+              (0, 1, 2), mixed_shapes) if has_mixed else None
     if not r or not wr:
         return None
     t = (r[0] + wr[0]) / 1e3
@@ -662,7 +665,8 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
         out["mixed_method"] = (f"{k} read streams and the write stream in ONE launch (mic_mixed_streams): each lane "
                                f"loads its 16-byte vector of all {k} inputs and stores input 0's back in place, no "
                                "arithmetic; the reduce's own access pattern and K:1 read:write interleave, best over "
-                               "the same shapes and flavours")
+                               "one-wave blocks at every residency 5-32 per CU and 256 / 1024-lane blocks, in the "
+                               "same flavours")
     return out
 
 
