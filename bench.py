@@ -775,19 +775,36 @@ def config_legs(m, stream, layout, launches=10):
     a = (rng.random(n, dtype=np.float32) * 2 - 1)
     b0 = (rng.random(n, dtype=np.float32) * 2 - 1)
     shim = _lib.shim()
-    b = b0.copy()
-    tt = []
-    for _ in range(200):
-        t0 = time.perf_counter()
-        _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0), "ccl_comp_reduce")
-        tt.append(time.perf_counter() - t0)
-    b = b0.copy()
-    _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0), "ccl_comp_reduce")
     exp = b0 + a  # IEEE RNE fp32 add, no NaNs in these inputs
+
+    def c1_times(sched_mode):
+        # sched_mode 1: a schedule without a stream, as nreduce's reduce
+        # entries pass it in a CPU oneCCL build (host memory, no lookup);
+        # 0: no schedule (operands looked up)
+        prev = shim.mi_ccl_comp_shim_sched(sched_mode)
+        try:
+            b = b0.copy()
+            tt = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0),
+                                "ccl_comp_reduce")
+                tt.append(time.perf_counter() - t0)
+            b = b0.copy()
+            _lib.check_shim(shim.mi_ccl_comp_reduce(a.ctypes.data, n, b.ctypes.data, None, 9, 0), "ccl_comp_reduce")
+        finally:
+            shim.mi_ccl_comp_shim_sched(prev)
+        return tt, int(np.count_nonzero(b.view(np.uint32) != exp.view(np.uint32)))
+
+    tt, mism = c1_times(1)
+    tt0, mism0 = c1_times(0)
     legs["c1"] = {"workload": "512 KiB fp32 sum chunk (nreduce of a 2-rank 1 MiB allreduce), host buffers through "
-                              "ccl_comp_reduce (the dispatcher keeps it on the calling thread's CPU)",
+                              "ccl_comp_reduce under a schedule without a stream (how a CPU oneCCL build's reduce "
+                              "entries call it: the calling thread's CPU, nothing looked up); timed from Python "
+                              "(ctypes call included)",
                   "median_us": round(statistics.median(tt) * 1e6, 2), "best_us": round(min(tt) * 1e6, 2),
-                  "parity": {"elements": n, "mismatches": int(np.count_nonzero(b.view(np.uint32) != exp.view(np.uint32)))}}
+                  "no_schedule_median_us": round(statistics.median(tt0) * 1e6, 2),
+                  "parity": {"elements": 2 * n, "mismatches": mism + mism0}}
     return legs
 
 
