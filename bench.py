@@ -217,12 +217,13 @@ class PinnedPool:
         self.done = threading.Barrier(self.n + 1)
         self.job = None
         self.errors = []
+        self.pin_errors = []  # reported, not raised: an unpinned thread still measures
 
         def body(i, cpu):
             try:
                 os.sched_setaffinity(0, {cpu})  # pid 0: the calling thread
             except OSError as e:
-                self.errors.append(f"pin cpu {cpu}: {e}")
+                self.pin_errors.append(f"pin cpu {cpu}: {e}")
             while True:
                 self.go.wait()
                 job = self.job
@@ -258,7 +259,8 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
     (so its pages sit on its own NUMA node), then reducing
     that range with the reference's loop: k - 1 chained 2-input calls, as
     CCL_WORKER_COUNT workers would each reduce their chunk.  Whole-bucket
-    reps repeated for ~`seconds`; returns (best GiB/s, median GiB/s, reps)."""
+    reps repeated for ~`seconds`; returns (best GiB/s, median GiB/s, reps,
+    the threads that could not be pinned)."""
     import ctypes
 
     import numpy as np
@@ -306,6 +308,7 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
                     oracle.comp_reduce(x[lo:hi], acc[lo:hi], dt, op)
 
     pool = PinnedPool(cpus)
+    pin_errors = pool.pin_errors
     try:
         pool.run(touch)
         pool.run(reduce)  # warm
@@ -318,7 +321,7 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
     finally:
         pool.close()
     del ins, acc
-    return bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times)
+    return bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times), list(pin_errors)
 
 
 def cpu_baseline(cfg, seconds):
@@ -352,7 +355,7 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
-    (b1, m1, r1) = res[1]
+    (b1, m1, r1, _) = res[1]
     # sanity probe, independent of the oracle: one core's memcpy bandwidth
     # over the same footprint (numpy's copy is a single-threaded memcpy)
     src = np.ones(bucket // 8, np.float64)
@@ -365,10 +368,11 @@ def cpu_baseline(cfg, seconds):
         ct.append(time.perf_counter() - t0)
     copy_gbps = 2 * src.nbytes / min(ct) / 1e9
     del src, dst
-    sweep = [{"threads": t, "best": round(b, 3), "median": round(m, 3), "reps": r,
-              "spread": round((b - m) / b, 4)} for t, (b, m, r) in sorted(res.items())]
+    sweep = [dict({"threads": t, "best": round(b, 3), "median": round(m, 3), "reps": r,
+                   "spread": round((b - m) / b, 4)}, **({"pin_errors": pe} if pe else {}))
+             for t, (b, m, r, pe) in sorted(res.items())]
     head = 16 if 16 in res else max(res)
-    bn, mn, rn = res[head]
+    bn, mn, rn, _ = res[head]
     return {
         "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "reference" if use_ref else "port",
         "traffic_GBps_1core": round(b1 * GiB * (k + 1) / 1e9, 1),
@@ -1046,8 +1050,12 @@ def main():
     if world > 1:
         dist.barrier()  # every rank is past its timed region before rank 0 loads the host cores
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, args.cpu_seconds)
-        if world > 1:
+        try:
+            cpu = cpu_baseline(cfg, args.cpu_seconds)
+        except Exception as e:  # noqa: BLE001 - a reported baseline never costs the line
+            cpu = {"error": f"{type(e).__name__}: {e}"}
+            log(f"cpu_baseline failed: {cpu['error']}")
+        if world > 1 and "error" not in cpu:
             cpu["note_n_gpus"] = (f"measured on rank 0 after the {world}-rank timed region and a barrier, while the "
                                   "other ranks idle; the same bounded sample as at N=1")
 

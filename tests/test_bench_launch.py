@@ -308,5 +308,6 @@ def test_cpu_sweep_point_pins_and_reduces():
     import os
     cfg = ("fp32 sum", 9, 4, 0, 2, 8 << 20, 0)
     cpus = sorted(os.sched_getaffinity(0))[:2]
-    b, m, r = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
+    b, m, r, pin_errors = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
+    assert pin_errors == []
     assert b >= m > 0 and r >= 5
