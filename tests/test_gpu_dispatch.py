@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 from oneccl_amd import comp
-from tests.util import BF16, FP32, assert_same, rand_array, to_dev, from_dev
+from tests.util import BF16, FP32, assert_same, rand_array, to_dev, from_dev, wait_os_threads_gone
 
 pytestmark = pytest.mark.gpu
 
@@ -269,6 +269,7 @@ def test_split_yields_to_concurrent_workers(limit, threshold):
         t.start()
     for t in ts:
         t.join()
+    assert wait_os_threads_gone([t.native_id for t in ts])
     assert not errs, errs
     if limit == "2":  # 4 workers > 2: nobody split
         assert all(s < 0 for s in shares), shares

@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 from oneccl_amd import _lib, comp
-from tests.util import BF16, FP32, assert_same, rand_array
+from tests.util import BF16, FP32, assert_same, rand_array, wait_os_threads_gone
 
 pytestmark = pytest.mark.gpu
 
@@ -178,6 +178,7 @@ def test_host_schedule_concurrent_workers_mixed_sizes():
         t.start()
     for t in ts:
         t.join()
+    assert wait_os_threads_gone([t.native_id for t in ts])
     assert errors == []
 
 

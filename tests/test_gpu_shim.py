@@ -15,7 +15,8 @@ import pytest
 import oracle
 from oneccl_amd import _lib, comp
 from tests import kat
-from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, FP32, FP64, OP_NAME, OPS, assert_same, from_dev, rand_array, to_dev
+from tests.util import ALL_DTYPES, BF16, DT_NAME, FP16, FP32, FP64, OP_NAME, OPS, assert_same, from_dev, rand_array, to_dev, \
+    wait_os_threads_gone
 
 pytestmark = pytest.mark.gpu
 
@@ -626,9 +627,11 @@ def test_concurrent_worker_stress():
     import torch
     b_impl, f_impl = impls()
     errs = []
+    tids = []
     n = 33_333
 
     def worker(t):
+        tids.append(threading.get_native_id())
         try:
             rng = np.random.default_rng(t)
             for it in range(40):
@@ -666,6 +669,7 @@ def test_concurrent_worker_stress():
     for x in th:
         x.join(timeout=240)
     assert not any(x.is_alive() for x in th), "a worker did not finish"
+    assert wait_os_threads_gone(tids), "a worker's thread teardown did not finish"
     assert not errs, errs[:3]
 
 

@@ -127,3 +127,21 @@ def to_dev(a: np.ndarray, pad_elems: int = 0, offset_elems: int = 0):
 def from_dev(t, like: np.ndarray, offset_elems: int = 0) -> np.ndarray:
     host = t.cpu().numpy().view(like.dtype)
     return host[offset_elems:offset_elems + like.size].copy()
+
+
+def wait_os_threads_gone(native_ids, timeout=60.0):
+    """Wait until the OS threads `native_ids` (threading.get_native_id() of
+    each) have exited.  Python's Thread.join() returns when the thread's
+    Python function ends, before the OS thread runs its thread_local
+    destructors -- for the library, each thread's HIP context teardown
+    (streams, staging buffers) -- so a GPU test that starts workers lets
+    those teardowns finish here rather than overlap the next test."""
+    import os
+    import time
+    t0 = time.monotonic()
+    pending = set(native_ids)
+    while pending and time.monotonic() - t0 < timeout:
+        pending = {t for t in pending if os.path.exists(f"/proc/self/task/{t}")}
+        if pending:
+            time.sleep(0.005)
+    return not pending
