@@ -380,7 +380,13 @@ int mi_set_max_blocks(int max_blocks);
  * a worker oneCCL pinned to one core do not share that core.  0 = helpers
  * inherit their creator's mask (MI_REDUCE_HELPER_AFFINITY=inherit).       */
 int mi_helper_cpu_count(void);
-/* Test hook: a library thread holds an exit guard (the section the exit
+/* Per-thread device contexts (two streams, staging and bounce buffers):
+ * *created = contexts built so far, *pooled = contexts of exited threads
+ * waiting in the pool for the next thread on their device.  A thread's exit
+ * makes no HIP call; its contexts are reused, never freed before the
+ * process ends.  Diagnostic.                                               */
+int mi_context_stats(size_t* created, size_t* pooled);
+/* Test hook:a library thread holds an exit guard (the section the exit
  * handler waits for) for hold_ms milliseconds, < 0 = forever.  The handler
  * waits at most MI_REDUCE_EXIT_WAIT_S seconds (default 60), then names the
  * section on stderr and ends the process with status 70.                  */

@@ -896,15 +896,14 @@ struct Drain {
 };
 
 // Process exit against threads that are still exiting or still working.  A
-// thread's contexts are freed by its thread_local destructors (hipFree of
-// the staging buffers synchronises the device and takes milliseconds), and
-// its staging worker (t_stage) finishes the thread's un-waited asynchronous
-// requests when the thread exits.  A host program may exit while either is
-// still going: Python's Thread.join(), for one, returns before the OS thread
-// has run its thread_local destructors.  The HIP runtime's own exit-time
-// teardown then pulls the device from under those calls (a SIGSEGV inside
-// libamdhip64 from __call_tls_dtors, profiles/round2_dispatch/
-// exit_crash_trace.txt).
+// thread's staging worker (t_stage) finishes the thread's un-waited
+// asynchronous requests when the thread exits.  A host program may exit
+// while that is still going: Python's Thread.join(), for one, returns before
+// the OS thread has run its thread_local destructors.  The HIP runtime's own
+// exit-time teardown then pulls the device from under those calls (a SIGSEGV
+// inside libamdhip64 from __call_tls_dtors, profiles/round2_dispatch/
+// exit_crash_trace.txt).  (A thread's contexts themselves make no HIP call
+// when it exits: they go back to a pool, see ThreadCtx.)
 //
 // So every such section -- a context teardown, and every job a staging
 // worker runs -- holds an ExitGuard while it makes HIP calls.  An exit
@@ -965,15 +964,52 @@ struct ExitGuard {
     ExitGuard& operator=(const ExitGuard&) = delete;
 };
 
+// A thread's contexts (streams, staging and bounce buffers) outlive it: when
+// the thread exits they go to a process-wide pool, and the next thread that
+// needs a context on that device takes one from there.  So a thread exit
+// makes no HIP call -- no hipFree / hipHostFree / hipStreamDestroy running
+// from __call_tls_dtors while other threads copy and launch (oneCCL's workers
+// are long-lived, but a caller that starts short-lived threads, as the test
+// suites do, would otherwise free and reallocate gigabytes of staging memory
+// per thread) -- and work a thread left queued on its streams stays ordered
+// before whatever the next owner queues there.  The pool holds at most as
+// many contexts per device as threads ever used one at once; they are freed
+// with the process.
+// The pool is never destroyed (a thread may exit while the process runs its
+// static destructors).
+struct CtxPool {
+    std::mutex mu;
+    std::vector<DevCtx*> free;
+};
+CtxPool& ctx_pool() {
+    static CtxPool* p = new CtxPool();
+    return *p;
+}
+std::atomic<size_t> g_ctx_created{0};
+
 struct ThreadCtx {
     std::vector<DevCtx*> devs;
     ~ThreadCtx() {
-        ExitGuard g("a thread's HIP context teardown");
-        if (g.entered)
-            for (DevCtx* d : devs) delete d;
+        CtxPool& p = ctx_pool();
+        std::lock_guard<std::mutex> lk(p.mu);
+        for (DevCtx* d : devs)
+            if (d) p.free.push_back(d);
+        devs.clear();
     }
 };
 thread_local ThreadCtx t_ctx;
+
+DevCtx* pooled_ctx(int device) {
+    CtxPool& p = ctx_pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    for (size_t i = p.free.size(); i-- > 0;)
+        if (p.free[i]->device == device) {
+            DevCtx* d = p.free[i];
+            p.free.erase(p.free.begin() + (long)i);
+            return d;
+        }
+    return nullptr;
+}
 std::once_flag g_exit_hook;
 
 // Register at_process_exit once, after the HIP runtime is initialised (a HIP
@@ -989,6 +1025,7 @@ void ensure_exit_hook() {
 int get_ctx(int device, DevCtx** out) {
     if (device < 0) MI_HIP(hipGetDevice(&device));
     if ((size_t)device >= t_ctx.devs.size()) t_ctx.devs.resize(device + 1, nullptr);
+    if (!t_ctx.devs[device]) t_ctx.devs[device] = pooled_ctx(device);
     if (!t_ctx.devs[device]) {
         // Built in full before it is published: a failure leaves no
         // half-made context (a null stream would be the legacy default
@@ -1006,6 +1043,7 @@ int get_ctx(int device, DevCtx** out) {
         d->device = device;
         for (int s = 0; s < 2; s++) MI_HIP(hipStreamCreateWithFlags(&d->stream[s], hipStreamNonBlocking));
         t_ctx.devs[device] = d.release();
+        g_ctx_created.fetch_add(1);
     }
     *out = t_ctx.devs[device];
     return 0;
@@ -2265,6 +2303,16 @@ const char* mi_last_error(void) { return g_last_error.c_str(); }
 int mi_version(void) { return 100; }  // 0.1.0
 
 int mi_helper_cpu_count(void) { return g_helper_cpus.use ? CPU_COUNT(&g_helper_cpus.mask) : 0; }
+
+int mi_context_stats(size_t* created, size_t* pooled) {
+    if (created) *created = g_ctx_created.load();
+    if (pooled) {
+        CtxPool& p = ctx_pool();
+        std::lock_guard<std::mutex> lk(p.mu);
+        *pooled = p.free.size();
+    }
+    return 0;
+}
 
 int mi_device_count(void) {
     int n = 0;

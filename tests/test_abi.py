@@ -207,3 +207,10 @@ def test_residency_override():
     assert m.mi_get_residency(-1, 8, ctypes.byref(w), None) == 0 and w.value == 9
     assert m.mi_set_residency(17, 8) == -1 and m.mi_set_residency(-1, 8) == -1
     assert m.mi_set_residency(2, 33) == -1 and m.mi_set_residency(2, -1) == -1
+
+
+def test_context_stats_need_no_device():
+    created, pooled = ctypes.c_size_t(99), ctypes.c_size_t(99)
+    assert _lib.mi().mi_context_stats(ctypes.byref(created), ctypes.byref(pooled)) == 0
+    assert created.value >= 0 and pooled.value <= created.value
+    assert _lib.mi().mi_context_stats(None, None) == 0

@@ -1,0 +1,75 @@
+"""Per-thread device contexts are pooled, not freed, when a thread exits
+(mi_reduce.hip, ThreadCtx): a thread's exit makes no HIP call, and the next
+thread on the device takes the exited thread's streams and staging buffers.
+Short-lived threads one after another then build at most one context, and
+each one's staged (pageable) reduce still gives the oracle's bits."""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from oneccl_amd import _lib
+from tests.util import FP32, assert_same, rand_array, wait_os_threads_gone
+
+pytestmark = pytest.mark.gpu
+
+
+def _stats():
+    created, pooled = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(_lib.mi().mi_context_stats(ctypes.byref(created), ctypes.byref(pooled)))
+    return created.value, pooled.value
+
+
+def _staged_reduce(seed, n, errs):
+    try:
+        m = _lib.mi()
+        a = rand_array(FP32, n, seed=seed, specials=False)
+        b = rand_array(FP32, n, seed=seed + 1, specials=False)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, FP32, 0)
+        _lib.check(m.mi_reduce_sync(a.ctypes.data, b.ctypes.data, n, FP32, 0, 0, -1))
+        assert_same(b, exp, FP32)
+    except Exception as e:  # noqa: BLE001
+        errs.append(e)
+
+
+def test_sequential_threads_reuse_one_context():
+    n = (3 << 20) // 4 + 7  # 3 MiB per operand: past the bounce buffers, staged
+    errs = []
+    created0, _ = _stats()
+    for t in range(6):
+        th = threading.Thread(target=_staged_reduce, args=(100 + 2 * t, n, errs))
+        th.start()
+        th.join()
+        assert wait_os_threads_gone([th.native_id])
+    created1, pooled1 = _stats()
+    assert not errs, errs[:3]
+    assert created1 - created0 <= 1, (created0, created1)
+    assert pooled1 >= 1
+
+
+def test_concurrent_threads_then_reuse():
+    n = (3 << 20) // 4 + 7
+    errs = []
+    ths = [threading.Thread(target=_staged_reduce, args=(300 + 2 * t, n, errs)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert wait_os_threads_gone([th.native_id for th in ths])
+    created1, pooled1 = _stats()
+    assert pooled1 >= 1  # the four threads' contexts (threads that ran apart shared one)
+    ths = [threading.Thread(target=_staged_reduce, args=(400 + 2 * t, n, errs)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert wait_os_threads_gone([th.native_id for th in ths])
+    created2, _ = _stats()
+    assert not errs, errs[:3]
+    # four threads at once take the pooled contexts first
+    assert created2 - created1 <= max(0, 4 - pooled1), (created1, pooled1, created2)
