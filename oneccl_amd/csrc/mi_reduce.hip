@@ -478,11 +478,25 @@ void publish_ranges(RangeSnap* next) {
 // `devptr` (optional): the device-visible address of a pinned host pointer.
 // `bytes`: the extent of the operand at p (for the declared ranges).
 PtrKind classify_hip(const void* p, int* dev, void** devptr);
+bool pinned_extent(uintptr_t a, intptr_t delta, uintptr_t* lo, uintptr_t* hi);
 
 PtrKind classify(const void* p, int* dev, void** devptr = nullptr, size_t bytes = 1) {
     PtrKind dk;
     if (declared(p, bytes ? bytes : 1, &dk, devptr)) return dk;
-    return classify_hip(p, dev, devptr);
+    void* dv = const_cast<void*>(p);
+    const PtrKind k = classify_hip(p, dev, &dv);
+    if (k == PK_PINNED && bytes > 1) {
+        // HIP answers for the first byte only.  The zero-copy kernel reads the
+        // whole operand in place, so a pinned operand must lie inside one
+        // pinned allocation (as mi_host_declare requires of a pinned range):
+        // one that runs on into pageable memory is staged instead of faulting.
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const intptr_t delta = (intptr_t)(reinterpret_cast<uintptr_t>(dv) - a);
+        uintptr_t lo = 0, hi = 0;
+        if (!pinned_extent(a, delta, &lo, &hi) || bytes > hi - a) return PK_PAGEABLE;
+    }
+    if (devptr) *devptr = dv;
+    return k;
 }
 
 // HIP's answer (one runtime lookup, counted for mi_pointer_lookups)
@@ -744,6 +758,7 @@ struct DevCtx {
     hipEvent_t ready[2] = {nullptr, nullptr};  // per slot: the chunk's result is in dbuf
     std::vector<void*> hbuf;                // pinned bounce buffers for small pageable operands
     size_t hbuf_bytes = 0;
+    char* edge = nullptr;                   // pinned scratch for the unaligned ends of D2H copies (Edges)
 
     ~DevCtx() {
         // Contexts die with their thread; device teardown at process exit may
@@ -755,8 +770,100 @@ struct DevCtx {
         }
         if (d2h) (void)hipStreamDestroy(d2h);
         for (void* p : hbuf) (void)hipHostFree(p);
+        if (edge) (void)hipHostFree(edge);
     }
 };
+
+// A copy the synchronous caller makes after the GPU is done (pinned -> `dst`).
+struct HostCopy {
+    void* dst = nullptr;
+    const void* src = nullptr;
+    size_t bytes = 0;
+};
+
+// ---- the runtime's copies of pageable memory ---------------------------------
+// The runtime's copies between pageable host memory and the device get
+// 16-byte-aligned host addresses and 16-byte multiples only.  On MI355X /
+// ROCm 7.2 an H2D copy from pageable memory whose source was 2-byte aligned
+// (a bf16 operand at an odd element offset of a packed buffer: oneCCL's tmp
+// buffer of peer chunks) faulted the GPU ("an illegal memory access") in two
+// of several full GPU-suite runs, both times at that one case -- the only
+// staged copy with such a source -- and never at the 4-byte-aligned fp32 cases
+// around it (profiles/round5_host/pytest_gpu_fault_run.txt,
+// profiles/round5_run8/).  The staged path's own kernels read only device
+// buffers, so the copy itself is the suspect; a fault that depends on where
+// the operand lies relative to a page would come and go exactly like this.
+// So:
+//  * H2D into a staging buffer copies the aligned span around the operand
+//    (h2d_stage).  Aligning down the start and up the end by < 16 bytes never
+//    leaves the pages the operand touches, so nothing unmapped is read; the
+//    kernel reads the operand `shift` bytes into the staging buffer.
+//  * D2H into pageable memory copies the aligned interior; the head and tail
+//    (< 16 bytes each) go to pinned scratch and are copied to the destination
+//    by the CPU after the stream is done (Edges, d2h_pageable).  Nothing
+//    outside the destination is written.
+constexpr uintptr_t kHostAlign = 16;
+constexpr size_t kStageSlack = 2 * kHostAlign;  // a staging buffer holds a chunk and its alignment
+inline uintptr_t host_align_dn(uintptr_t a) { return a & ~(kHostAlign - 1); }
+inline uintptr_t host_align_up(uintptr_t a) { return (a + kHostAlign - 1) & ~(kHostAlign - 1); }
+
+hipError_t h2d_stage(void* dst, const void* src, size_t bytes, hipStream_t s, size_t* shift) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+    const uintptr_t lo = host_align_dn(a), hi = host_align_up(a + bytes);
+    *shift = a - lo;
+    return hipMemcpyAsync(dst, reinterpret_cast<const void*>(lo), hi - lo, hipMemcpyHostToDevice, s);
+}
+
+constexpr size_t kEdgeBytes = 8192;            // DevCtx::edge
+constexpr size_t kEdgeSlot = 2 * kHostAlign;   // one D2H: head + tail
+constexpr size_t kDrainEdge = kEdgeBytes - kEdgeSlot;  // the drain thread's slot (the last one)
+
+struct Edges {
+    char* pin = nullptr;  // pinned scratch, kEdgeSlot bytes per D2H
+    size_t slots = 0, used = 0;
+    std::vector<HostCopy> post;
+    bool full() const { return used >= slots; }
+    // after the stream(s) carrying the D2H copies are done
+    void flush() {
+        for (const HostCopy& c : post) memcpy(c.dst, c.src, c.bytes);
+        post.clear();
+        used = 0;
+    }
+};
+
+int ensure_edges(DevCtx* d) {
+    if (!d->edge) {
+        void* p = nullptr;
+        MI_HIP(hipHostMalloc(&p, kEdgeBytes, hipHostMallocDefault));
+        d->edge = static_cast<char*>(p);
+    }
+    return 0;
+}
+
+// D2H of device [src, src + bytes) into pageable host memory at dst; needs a
+// free slot in `e` (the caller flushes a full one first).
+hipError_t d2h_pageable(void* dst, const void* src, size_t bytes, hipStream_t s, Edges& e) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
+    const size_t head = std::min(bytes, (size_t)(host_align_up(a) - a));
+    const size_t interior = (bytes - head) & ~(size_t)(kHostAlign - 1);
+    const size_t tail = bytes - head - interior;
+    const char* s8 = static_cast<const char*>(src);
+    char* d8 = static_cast<char*>(dst);
+    hipError_t r = hipSuccess;
+    if (interior) r = hipMemcpyAsync(d8 + head, s8 + head, interior, hipMemcpyDeviceToHost, s);
+    if (head || tail) {
+        char* slot = e.pin + kEdgeSlot * e.used++;
+        if (r == hipSuccess && head) {
+            r = hipMemcpyAsync(slot, s8, head, hipMemcpyDeviceToHost, s);
+            e.post.push_back(HostCopy{d8, slot, head});
+        }
+        if (r == hipSuccess && tail) {
+            r = hipMemcpyAsync(slot + kHostAlign, s8 + head + interior, tail, hipMemcpyDeviceToHost, s);
+            e.post.push_back(HostCopy{d8 + head + interior, slot + kHostAlign, tail});
+        }
+    }
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // where helper threads run
@@ -845,13 +952,17 @@ struct Drain {
     hipError_t err = hipSuccess;
     std::thread th;
 
-    void start(int device, hipStream_t s) {
+    // `edge`: pinned scratch for the unaligned ends of its D2H copies (kEdgeSlot bytes)
+    void start(int device, hipStream_t s, char* edge) {
         if (th.joinable()) return;
-        th = std::thread([this, device, s] { loop(device, s); });
+        th = std::thread([this, device, s, edge] { loop(device, s, edge); });
     }
-    void loop(int device, hipStream_t s) {
+    void loop(int device, hipStream_t s, char* edge) {
         helper_thread_affinity();
         hipError_t e = hipSetDevice(device);
+        Edges ed;
+        ed.pin = edge;
+        ed.slots = 1;
         for (;;) {
             Task t;
             {
@@ -862,8 +973,11 @@ struct Drain {
                 q.pop_front();
             }
             if (e == hipSuccess) e = hipEventSynchronize(t.ready);
-            if (e == hipSuccess) e = hipMemcpyAsync(t.dst, t.src, t.bytes, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = d2h_pageable(t.dst, t.src, t.bytes, s, ed);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) ed.flush();
+            ed.post.clear();
+            ed.used = 0;
             std::lock_guard<std::mutex> lk(mu);
             if (e != hipSuccess && err == hipSuccess) err = e;
             done++;
@@ -1067,12 +1181,14 @@ int ensure_bounce(DevCtx* d, size_t nbuf) {
 
 int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
     if (d->dbuf[0].size() >= nbuf && d->dbuf_bytes >= bytes) return 0;
+    // grow to the larger of the old and the new shape (a call with fewer but
+    // larger operands keeps room for the earlier call's operand count)
+    const size_t want = std::max(bytes, d->dbuf_bytes);
+    nbuf = std::max(nbuf, d->dbuf[0].size());
     for (int s = 0; s < 2; s++) {
         for (void* p : d->dbuf[s]) MI_HIP(hipFree(p));
         d->dbuf[s].clear();
     }
-    const size_t want = std::max(bytes, d->dbuf_bytes);
-    nbuf = std::max(nbuf, d->dbuf[0].size());
     d->dbuf_bytes = 0;  // published only once every buffer exists: a failed
                         // hipMalloc leaves no null slot behind for the next call
     for (int s = 0; s < 2; s++) {
@@ -1092,16 +1208,9 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
 // bit 1: stream[1]).  All-device or zero-copy: one launch on stream[0].
 // Otherwise: chunks of kChunkBytes, two pipeline slots on two streams (H2D
 // of chunk c+1 overlaps the kernel / D2H of chunk c).
-// A copy the synchronous caller makes after the GPU is done (bounce -> `out`).
-struct HostCopy {
-    void* dst = nullptr;
-    const void* src = nullptr;
-    size_t bytes = 0;
-};
-
 int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
                  unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr,
-                 HostCopy* post = nullptr, hipEvent_t* t_start = nullptr) {
+                 std::vector<HostCopy>* post = nullptr, hipEvent_t* t_start = nullptr) {
     *ctx = nullptr;
     *used = 0;
     const size_t es = dtype_size(dt);
@@ -1193,7 +1302,7 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         *used = 1;
         rc = launch_reduce(bins, k, bout, count, dt, op, flags, d->stream[0], true);
         if (rc) return rc;
-        if (kout == PK_PAGEABLE) *post = HostCopy{out, bout, count * es};
+        if (kout == PK_PAGEABLE) post->push_back(HostCopy{out, bout, count * es});
         return 0;
     }
 
@@ -1216,17 +1325,30 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     }
     size_t chunk_elems = kChunkBytes / es;
     chunk_elems -= chunk_elems % 16;  // keeps VCVTNEPS2BF16-tail split aligned (see below)
-    rc = ensure_scratch(d, (size_t)nhost, chunk_elems * es);
+    // each host operand sits at its own 16-byte offset in its staging buffers
+    // (h2d_stage); chunk starts are 16-byte multiples apart, so every chunk
+    // keeps it
+    size_t shift[MI_MAX_INPUTS + 1];
+    for (int j = 0; j < nhost; j++) shift[j] = reinterpret_cast<uintptr_t>(host_ptr[j]) & (kHostAlign - 1);
+    rc = ensure_scratch(d, (size_t)nhost, chunk_elems * es + kStageSlack);
     if (rc) return rc;
 
     const size_t nchunks = (count + chunk_elems - 1) / chunk_elems;
     *used = nchunks > 1 ? 3 : 1;
-    const bool drained = drain && kout == PK_PAGEABLE && slot_of[k] >= 0 && nchunks > 1;
+    const bool d2h_pg = kout == PK_PAGEABLE && slot_of[k] >= 0;
+    const bool drained = drain && d2h_pg && nchunks > 1;
+    Edges edges;  // unaligned ends of the D2H copies this thread issues
+    if (d2h_pg) {
+        rc = ensure_edges(d);
+        if (rc) return rc;
+        edges.pin = d->edge;
+        edges.slots = kDrainEdge / kEdgeSlot;
+    }
     if (drained) {
         if (!d->d2h) MI_HIP(hipStreamCreateWithFlags(&d->d2h, hipStreamNonBlocking));
         for (int s = 0; s < 2; s++)
             if (!d->ready[s]) MI_HIP(hipEventCreateWithFlags(&d->ready[s], hipEventDisableTiming));
-        drain->start(d->device, d->d2h);
+        drain->start(d->device, d->d2h, d->edge + kDrainEdge);
     }
     for (size_t c = 0; c < nchunks; c++) {
         const int s = (int)(c & 1);
@@ -1242,16 +1364,17 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
             if (slot_of[i] < 0) {
                 din[i] = static_cast<const char*>(inputs[i]) + off * es;
             } else {
-                void* buf = d->dbuf[s][slot_of[i]];
+                char* buf = static_cast<char*>(d->dbuf[s][slot_of[i]]);
                 if (!loaded[slot_of[i]]) {
-                    MI_HIP(hipMemcpyAsync(buf, static_cast<const char*>(inputs[i]) + off * es, bytes,
-                                          hipMemcpyHostToDevice, st));
+                    size_t sh = 0;
+                    MI_HIP(h2d_stage(buf, static_cast<const char*>(inputs[i]) + off * es, bytes, st, &sh));
                     loaded[slot_of[i]] = true;
                 }
-                din[i] = buf;
+                din[i] = buf + shift[slot_of[i]];
             }
         }
-        void* cdst = (slot_of[k] < 0) ? static_cast<char*>(out) + off * es : d->dbuf[s][slot_of[k]];
+        void* cdst = (slot_of[k] < 0) ? static_cast<char*>(out) + off * es
+                                      : static_cast<char*>(d->dbuf[s][slot_of[k]]) + shift[slot_of[k]];
         // The tail-truncation split is defined on the whole array: only the
         // last chunk holds elements >= (count/16)*16, and chunk starts are
         // multiples of 16, so the per-chunk split computed inside
@@ -1259,12 +1382,27 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         rc = launch_reduce(din, k, cdst, n, dt, op, flags, st, true);
         if (rc) return rc;
         if (slot_of[k] >= 0) {
+            void* hdst = static_cast<char*>(out) + off * es;
             if (drained) {
                 MI_HIP(hipEventRecord(d->ready[s], st));
-                drain->push({static_cast<char*>(out) + off * es, cdst, bytes, d->ready[s]});
+                drain->push({hdst, cdst, bytes, d->ready[s]});
+            } else if (d2h_pg) {
+                if (edges.full()) {  // every slot holds an end not yet copied out
+                    for (int q = 0; q < 2; q++) MI_HIP(wait_stream(d->stream[q]));
+                    edges.flush();
+                }
+                MI_HIP(d2h_pageable(hdst, cdst, bytes, st, edges));
             } else {
-                MI_HIP(hipMemcpyAsync(static_cast<char*>(out) + off * es, cdst, bytes, hipMemcpyDeviceToHost, st));
+                MI_HIP(hipMemcpyAsync(hdst, cdst, bytes, hipMemcpyDeviceToHost, st));
             }
+        }
+    }
+    if (!edges.post.empty()) {
+        if (post) {  // copied by the synchronous caller after its wait
+            post->insert(post->end(), edges.post.begin(), edges.post.end());
+        } else {
+            for (int q = 0; q < 2; q++) MI_HIP(wait_stream(d->stream[q]));
+            edges.flush();
         }
     }
     return 0;
@@ -1275,14 +1413,14 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     DevCtx* d = nullptr;
     int used = 0;
     Drain drain;
-    HostCopy post;
+    std::vector<HostCopy> post;
     const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain, &post);
     const hipError_t de = drain.finish();  // every staged result is in `out` after this
     if (rc) return rc;
     if (de != hipSuccess) return hip_fail(de, "staged D2H into pageable memory");
     for (int s = 0; s < 2; s++)
         if (used & (1 << s)) MI_HIP(wait_stream(d->stream[s]));
-    if (post.bytes) memcpy(post.dst, post.src, post.bytes);
+    for (const HostCopy& c : post) memcpy(c.dst, c.src, c.bytes);
     return 0;
 }
 
@@ -1683,8 +1821,15 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
         const size_t ss = dtype_size(src_dtype), ds = dtype_size(dst_dtype);
         size_t chunk = kChunkBytes / std::max(ss, ds);
         chunk -= chunk % 16;
-        rc = ensure_scratch(d, 2, chunk * std::max(ss, ds));
+        rc = ensure_scratch(d, 2, chunk * std::max(ss, ds) + kStageSlack);
         if (rc) return rc;
+        Edges edges;  // unaligned ends of D2H copies into pageable memory (d2h_pageable)
+        if (kd == PK_PAGEABLE) {
+            rc = ensure_edges(d);
+            if (rc) return rc;
+            edges.pin = d->edge;
+            edges.slots = kDrainEdge / kEdgeSlot;
+        }
         for (size_t off = 0, c = 0; off < count; off += chunk, c++) {
             const int sl = (int)(c & 1);
             hipStream_t st = d->stream[sl];
@@ -1694,18 +1839,30 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
             const void* dsrc = sp;
             void* ddst = dp;
             if (ks != PK_DEVICE) {
-                MI_HIP(hipMemcpyAsync(d->dbuf[sl][0], sp, n * ss, hipMemcpyHostToDevice, st));
-                dsrc = d->dbuf[sl][0];
+                size_t sh = 0;
+                MI_HIP(h2d_stage(d->dbuf[sl][0], sp, n * ss, st, &sh));
+                dsrc = static_cast<const char*>(d->dbuf[sl][0]) + sh;
             }
-            if (kd != PK_DEVICE) ddst = d->dbuf[sl][1];
+            if (kd != PK_DEVICE)
+                ddst = static_cast<char*>(d->dbuf[sl][1]) + (reinterpret_cast<uintptr_t>(dp) & (kHostAlign - 1));
             // chunk starts are multiples of 16: the tail split is the global one
             rc = launch_convert(dsrc, src_dtype, ddst, dst_dtype, n, flags, st,
                                 trunc_from > off ? std::min<uint64_t>(trunc_from - off, n) : 0);
             if (rc) return rc;
-            if (kd != PK_DEVICE) MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
+            if (kd == PK_PAGEABLE) {
+                if (edges.full()) {
+                    MI_HIP(wait_stream(d->stream[0]));
+                    MI_HIP(wait_stream(d->stream[1]));
+                    edges.flush();
+                }
+                MI_HIP(d2h_pageable(dp, ddst, n * ds, st, edges));
+            } else if (kd != PK_DEVICE) {
+                MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
+            }
         }
         MI_HIP(wait_stream(d->stream[0]));
         MI_HIP(wait_stream(d->stream[1]));
+        edges.flush();
         return 0;
     });
 }
@@ -2063,8 +2220,53 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
             if (prev != d->device) (void)hipSetDevice(prev);
             return rc;
         }
-        MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, d->stream[0]));
-        MI_HIP(wait_stream(d->stream[0]));
+        if (ks != PK_DEVICE && kd != PK_DEVICE) {  // host to host: the CPU's copy
+            memcpy(dst, src, bytes);
+            return 0;
+        }
+        int prev = 0;
+        MI_HIP(hipGetDevice(&prev));
+        if (prev != d->device) MI_HIP(hipSetDevice(d->device));
+        struct Restore {
+            int dev, cur;
+            ~Restore() {
+                if (dev != cur) (void)hipSetDevice(dev);
+            }
+        } restore{prev, d->device};
+        hipStream_t st = d->stream[0];
+        if (ks == PK_PAGEABLE || kd == PK_PAGEABLE) {  // the runtime gets aligned host spans only (h2d_stage)
+            rc = ensure_edges(d);
+            if (rc) return rc;
+            Edges edges;
+            edges.pin = d->edge;
+            edges.slots = 1;
+            if (kd == PK_PAGEABLE) {
+                MI_HIP(d2h_pageable(dst, src, bytes, st, edges));
+                MI_HIP(wait_stream(st));
+                edges.flush();
+                return 0;
+            }
+            // pageable -> device: the ends through pinned scratch, the aligned interior direct
+            const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+            const size_t head = std::min(bytes, (size_t)(host_align_up(a) - a));
+            const size_t interior = (bytes - head) & ~(size_t)(kHostAlign - 1);
+            const size_t tail = bytes - head - interior;
+            const char* s8 = static_cast<const char*>(src);
+            char* d8 = static_cast<char*>(dst);
+            if (head) {
+                memcpy(edges.pin, s8, head);
+                MI_HIP(hipMemcpyAsync(d8, edges.pin, head, hipMemcpyHostToDevice, st));
+            }
+            if (interior) MI_HIP(hipMemcpyAsync(d8 + head, s8 + head, interior, hipMemcpyHostToDevice, st));
+            if (tail) {
+                memcpy(edges.pin + kHostAlign, s8 + head + interior, tail);
+                MI_HIP(hipMemcpyAsync(d8 + head + interior, edges.pin + kHostAlign, tail, hipMemcpyHostToDevice, st));
+            }
+            MI_HIP(wait_stream(st));
+            return 0;
+        }
+        MI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+        MI_HIP(wait_stream(st));
         return 0;
     });
 }
@@ -2113,6 +2315,7 @@ const char* mi_reduction_to_str(int op) {
 // allocation is the one mi_host_register pinned, or the one HIP reports for
 // the address (hipHostMalloc / a caller's own hipHostRegister).  Anything
 // else is recorded as pageable, which is always safe: it is staged.
+namespace {
 std::mutex g_reg_mu;
 std::map<uintptr_t, size_t> g_registered;  // mi_host_register: base -> bytes, under g_reg_mu
 
@@ -2166,6 +2369,7 @@ void demote_declared(uintptr_t lo, uintptr_t hi) {
         }
     publish_ranges(next.release());
 }
+}  // namespace
 
 int mi_host_register(void* ptr, size_t bytes) {
     if (!ptr || !bytes) return fail(MI_E_INVALID, "null / empty buffer");

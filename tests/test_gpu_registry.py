@@ -257,3 +257,38 @@ def test_unregistering_a_declared_pinned_buffer_demotes_it(gpu_dispatch, n):
             assert m.mi_host_undeclare(x.ctypes.data) == 0
     assert_same(b, exp, FP32)
     del raw_a, raw_b
+
+
+def test_operand_running_past_a_pinned_allocation_is_staged():
+    """HIP classifies a pointer by its first byte.  An operand that starts in
+    a pinned (registered) allocation and runs on into pageable pages must not
+    go to the zero-copy kernel, which would read the pageable pages in place
+    and fault the GPU: classify() checks the pinned allocation's extent and
+    stages such an operand.  The kinds are asserted before any GPU call."""
+    m = _lib.mi()
+    raw, buf = _page_aligned(8 * PAGE)
+    p = buf.ctypes.data
+    assert m.mi_host_register(p, 4 * PAGE) == 0
+    try:
+        dev = ctypes.c_int(-1)
+        assert m.mi_pointer_kind_range(p, 4 * PAGE, ctypes.byref(dev)) == 1  # inside the registration
+        assert m.mi_pointer_kind_range(p + 64, 4 * PAGE - 64, ctypes.byref(dev)) == 1
+        assert m.mi_pointer_kind_range(p, 4 * PAGE + 4, ctypes.byref(dev)) == 2  # one element past it
+        assert m.mi_pointer_kind_range(p, 8 * PAGE, ctypes.byref(dev)) == 2
+        n = 8 * PAGE // 4
+        a = buf.view(np.float32)
+        a[:] = rand_array(FP32, n, seed=21, specials=False)
+        b = rand_array(FP32, n, seed=22, specials=False)
+        exp = b.copy()
+        oracle.comp_reduce(a.copy(), exp, FP32, 0, *_impls())
+        _lib.check(m.mi_reduce_sync(a.ctypes.data, b.ctypes.data, n, FP32, 0, 0, -1))
+        assert_same(b, exp, FP32)
+        # and as the accumulator
+        c = rand_array(FP32, n, seed=23, specials=False)
+        exp2 = a.copy()
+        oracle.comp_reduce(c, exp2, FP32, 0, *_impls())
+        _lib.check(m.mi_reduce_sync(c.ctypes.data, a.ctypes.data, n, FP32, 0, 0, -1))
+        assert_same(a, exp2, FP32)
+    finally:
+        assert m.mi_host_unregister(p) == 0
+    del raw
