@@ -1019,13 +1019,11 @@ struct Drain {
 // exit_crash_trace.txt).  (A thread's contexts themselves make no HIP call
 // when it exits: they go back to a pool, see ThreadCtx.)
 //
-// So every such section -- a context teardown, and every job a staging
-// worker runs -- holds an ExitGuard while it makes HIP calls.  An exit
-// handler, registered after the runtime's (at the first context, when HIP is
-// initialised, so it runs before the runtime's), marks the process as
-// exiting and then waits until no guard is held.  A section that would start
-// after that mark makes no HIP call: a teardown leaves its context to the
-// process's end, a job fails with MI_E_EXITING.  The counter is raised before
+// So every job a staging worker runs holds an ExitGuard while it makes HIP
+// calls.  An exit handler, registered after the runtime's (at the first
+// context, when HIP is initialised, so it runs before the runtime's), marks
+// the process as exiting and then waits until no guard is held.  A job that
+// would start after that mark makes no HIP call: it fails with MI_E_EXITING.  The counter is raised before
 // the mark is read (both sequentially consistent), so either the section sees
 // the mark or the handler sees the section.
 //
