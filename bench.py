@@ -52,6 +52,15 @@ CONFIGS = {
 DTYPE_LABEL = {9: "f32", 11: "bf16 (f32 math)", 8: "f16 (f32 math)", 4: "int32", 6: "int64"}
 
 
+def mem_mark(tag):
+    """MI_BENCH_MEM_TRACE=1: the device bytes torch holds now and its peak so
+    far, per phase (checks memory_plan against what the phases allocate)."""
+    if os.environ.get("MI_BENCH_MEM_TRACE"):
+        import torch
+        log(f"mem {tag}: allocated {torch.cuda.memory_allocated() >> 20} MiB, "
+            f"peak {torch.cuda.max_memory_allocated() >> 20} MiB")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -426,12 +435,22 @@ def input_bytes(k, n, es, layout):
     return k * n * es
 
 
-def parity_bytes(n, dt, es):
-    """Device temporaries of full_parity: the torch fold (expected_result) --
-    the accumulator and its sum, and for bf16/fp16 the widened input and the
-    storage rounding's round trip in fp32 -- plus the mismatch mask (one byte
-    per element)."""
-    return (n * 4 * 4 + n * es if dt in (8, 11) else 2 * n * es) + n
+PARITY_CHUNK = 1 << 24  # elements per mismatch count (count_mismatches)
+
+
+def parity_bytes(n, dt, es, flags=0):
+    """Device temporaries of full_parity: the torch fold (expected_result:
+    the accumulator, folded in place; for bf16/fp16 an fp32 accumulator and
+    one widened input, then the rounding: an int32 shift and the storage copy
+    for bf16 truncation, the storage copy otherwise), then the expected result
+    beside one chunk's mismatch mask and its int64 count (9 bytes per element
+    of a chunk).  Measured equal with MI_BENCH_MEM_TRACE=1."""
+    if dt in (8, 11):
+        trunc = dt == 11 and not (flags & 0x2)
+        fold = max(8 * n, (4 + 4 + es) * n if trunc else (4 + es) * n)
+    else:
+        fold = es * n
+    return max(fold, es * n + 9 * min(n, PARITY_CHUNK))
 
 
 def memory_plan(config, layout, world, rank, scaling="weak"):
@@ -449,7 +468,7 @@ def memory_plan(config, layout, world, rank, scaling="weak"):
     n, _, _ = plan(n_total, es, rank, world, scaling)
     lay = "tmpbuf" if config == "c4-tmpbuf" else layout
     head = input_bytes(k, n, es, lay)
-    parity = parity_bytes(n, dt, es)
+    parity = parity_bytes(n, dt, es, flags)
     out = {"config": config, "layout": lay, "world": world, "rank": rank, "elements": n,
            "headline_inputs_bytes": head, "parity_temporaries_bytes": parity}
     peak = head + parity
@@ -458,10 +477,10 @@ def memory_plan(config, layout, world, rank, scaling="weak"):
         legs = {}
         for name in ("c3-bf16", "c3-fp16", "c4", "c4-tmpbuf", "c4-bf16acc", "c5-int32-max", "c5-int64-prod",
                      "c2-layout-one", "c2-layout-separate"):
-            _, ldt, les, _, lk, lbucket, _ = CONFIGS["c2" if name.startswith("c2-") else name]
+            _, ldt, les, _, lk, lbucket, lflags = CONFIGS["c2" if name.startswith("c2-") else name]
             ln = lbucket // les
             llay = "tmpbuf" if name == "c4-tmpbuf" else name[len("c2-layout-"):] if name.startswith("c2-") else layout
-            legs[name] = input_bytes(lk, ln, les, llay) + parity_bytes(ln, ldt, les)
+            legs[name] = input_bytes(lk, ln, les, llay) + parity_bytes(ln, ldt, les, lflags)
         out["config_legs_bytes"] = legs
         peak = max(peak, head + max(legs.values()))
     if world > 1 and config == "c2":
@@ -487,18 +506,19 @@ def expected_result(ins, k, dt, op, flags):
     import torch
     lp = dt in (8, 11)
     acc = ins[0].float() if lp else ins[0].clone()
-    for j in range(1, k):
+    for j in range(1, k):  # in place: one accumulator, one widened input at a time (parity_bytes)
         x = ins[j].float() if lp else ins[j]
         if op == 0:
-            acc = acc + x
+            acc.add_(x)
         elif op == 1:
-            acc = acc * x
+            acc.mul_(x)
         elif op == 2:
-            acc = torch.minimum(x, acc)
+            torch.minimum(x, acc, out=acc)
         else:
-            acc = torch.maximum(x, acc)
+            torch.maximum(x, acc, out=acc)
+        del x
         if lp and not (flags & 0x4):
-            acc = to_storage(acc, dt, flags).float()  # storage precision after every step
+            acc.copy_(to_storage(acc, dt, flags))  # storage precision after every step
     return to_storage(acc, dt, flags) if lp else acc
 
 
@@ -524,9 +544,14 @@ def count_mismatches(got, exp):
     """Elements whose bits differ (NaN payloads included)."""
     import torch
     ib = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[got.element_size()]
-    # count_nonzero reads the bool mask as is (a .sum() of it made an int64
-    # copy: 8 bytes per element, 2 GiB for the headline bucket)
-    return int(torch.count_nonzero(torch.ne(got.view(ib), exp.view(ib))).item())
+    g, e = got.reshape(-1).view(ib), exp.reshape(-1).view(ib)
+    # in chunks: counting a whole bucket's mask makes an int64 copy of it
+    # (8 bytes per element, 2 GiB for the headline bucket; measured with
+    # MI_BENCH_MEM_TRACE); a chunk bounds the temporaries (PARITY_CHUNK)
+    total = 0
+    for i in range(0, g.numel(), PARITY_CHUNK):
+        total += int(torch.count_nonzero(torch.ne(g[i:i + PARITY_CHUNK], e[i:i + PARITY_CHUNK])).item())
+    return total
 
 
 def full_parity(run_once, ins, k, dt, op, flags, seed0, entry):
@@ -736,8 +761,8 @@ def config_legs(m, stream, layout, launches=10):
             ins = alloc_tmpbuf(k, n, torch_dtype(dt))
         else:
             ins = alloc_inputs(k, n, torch_dtype(dt), c2_other.get(name, layout))
-        for j, t in enumerate(ins):
-            fill(t, 0xC0 + 131 * j)
+        for j in range(k):  # (no loop variable left holding a view: `del ins` frees the leg)
+            fill(ins[j], 0xC0 + 131 * j)
         arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
 
         def step():
@@ -978,8 +1003,8 @@ def main():
         ins = alloc_tmpbuf(k, n, tdt)
     else:
         ins = alloc_inputs(k, n, tdt, args.layout)
-    for j, t in enumerate(ins):
-        fill(t, 0xC0FFEE + 7919 * rank + j)
+    for j in range(len(ins)):  # (no loop variable left holding a view: `del ins` frees the bucket)
+        fill(ins[j], 0xC0FFEE + 7919 * rank + j)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     arr = _lib.void_ptr_array([t.data_ptr() for t in ins])
@@ -989,11 +1014,14 @@ def main():
             return m.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)  # inout += in
         return m.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
 
+    mem_mark("inputs")
     elapsed, avg_kern_ms, kern_ms = timed_steps(step, args.steps, args.warmup, stream, world)
     elapsed, avg_kern_ms_max = max_over_ranks([elapsed, avg_kern_ms], world, coll_dev)
+    mem_mark("timed")
     # the achievable ceiling on these buffers (outside the timed region;
     # overwrites ins[0], which full_parity refills)
     ceil = measured_ceiling(ins, k, n * es, stream)
+    mem_mark("ceiling")
 
     # the whole bucket checked bit for bit, outside the timed region (every
     # rank checks its own; the line reports the sum over ranks)
@@ -1033,6 +1061,7 @@ def main():
                 lambda: _lib.check_shim(shim.mi_ccl_comp_reduce(ins[1].data_ptr(), n, ins[0].data_ptr(), None, dt,
                                                                 op), "ccl_comp_reduce"),
                 ins, k, dt, op, shim_flags(dt), seed0 + 101, "ccl_comp_reduce")
+    mem_mark("parity + drop-in")
 
     # totals over ranks (each rank checked its own bucket shard)
     parity["elements"], parity["mismatches"] = (int(x) for x in sum_over_ranks(
@@ -1070,11 +1099,14 @@ def main():
     if world > 1 and args.config == "c2":
         strong = {"c2": strong_split(m, dt, es, op, k, flags, n_total, rank, world, stream, args.steps,
                                      args.warmup, coll_dev, ins=ins, n_devices=n_devices)}
+        mem_mark("strong c2")
         del ins
         torch.cuda.empty_cache()
+        mem_mark("headline freed")
         strong["c4_fanin8"] = strong_split(m, 9, 4, 0, 8, 0, GiB // 4, rank, world, stream, args.steps,
                                            args.warmup, coll_dev, n_devices=n_devices, layout=args.layout)
         torch.cuda.empty_cache()
+        mem_mark("strong c4")
 
     traffic = pmc_traffic(args.config, traffic_per_launch)
     mplan = memory_plan(args.config, args.layout, world, rank, args.scaling)

@@ -291,7 +291,40 @@ def test_memory_plan_layouts_and_tmpbuf():
     p = bench.memory_plan("c4-tmpbuf", "padded", 1, 0)
     assert p["layout"] == "tmpbuf" and p["headline_inputs_bytes"] == 8 * GIB
     p = bench.memory_plan("c3-bf16", "padded", 1, 0)
-    assert p["parity_temporaries_bytes"] == (128 << 20) * (4 * 4 + 2 + 1)  # fp32 fold temporaries, result, mask
+    # fp32 accumulator + one widened input (the fold is in place; RNE rounding: + the storage copy, less)
+    assert p["parity_temporaries_bytes"] == (128 << 20) * (4 + 4)
+    assert bench.parity_bytes(128 << 20, 11, 2, 0) == (128 << 20) * (4 + 4 + 2)  # truncation: int32 shift too
+    p = bench.memory_plan("c2", "padded", 1, 0)  # the accumulator; then result + one chunk's mask and count
+    assert p["parity_temporaries_bytes"] == GIB + 9 * bench.PARITY_CHUNK
+
+
+@pytest.mark.parametrize("dt,flags", [(9, 0), (4, 0), (6, 0), (11, 0), (11, 0x2), (11, 0x6), (8, 0), (8, 0x4)])
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_expected_result_in_place_fold_and_chunked_count(dt, flags, op, monkeypatch):
+    """bench.expected_result folds in place; its bits equal the out-of-place
+    left fold (CPU tensors), and count_mismatches counts in chunks."""
+    import torch
+    monkeypatch.setattr(bench, "PARITY_CHUNK", 1000)
+    n, k = 4099, 4
+    g = torch.Generator().manual_seed(dt * 10 + op)
+    tdt = bench.torch_dtype(dt)
+    if tdt.is_floating_point:
+        ins = [(torch.rand(n, generator=g) * 4 - 2).to(tdt) for _ in range(k)]
+    else:
+        ins = [torch.randint(-50, 50, (n,), generator=g).to(tdt) for _ in range(k)]
+    got = bench.expected_result(ins, k, dt, op, flags)
+    lp = dt in (8, 11)
+    acc = ins[0].float() if lp else ins[0].clone()
+    for j in range(1, k):
+        x = ins[j].float() if lp else ins[j]
+        acc = [acc + x, acc * x, torch.minimum(x, acc), torch.maximum(x, acc)][op]
+        if lp and not (flags & 0x4):
+            acc = bench.to_storage(acc, dt, flags).float()
+    ref = bench.to_storage(acc, dt, flags) if lp else acc
+    assert bench.count_mismatches(got, ref) == 0
+    bad = ref.clone()
+    bad.view(torch.uint8)[::977] ^= 1
+    assert bench.count_mismatches(bad, ref) == len(range(0, bad.numel() * bad.element_size(), 977))
 
 
 def test_core_plan_one_cpu_per_physical_core():
