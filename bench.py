@@ -1223,10 +1223,69 @@ def _host_pair(kind, nbytes):
     return a, b, a.ctypes.data, b.ctypes.data
 
 
+def gpu_numa_node(index=None):
+    """NUMA node of the GPU's PCI device (sysfs), or None."""
+    import torch
+    p = torch.cuda.get_device_properties(torch.cuda.current_device() if index is None else index)
+    dom, bus, dev = (getattr(p, a, -1) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if min(dom, bus, dev) < 0:
+        return None
+    try:
+        node = int(Path(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dev:02x}.0/numa_node").read_text())
+    except (OSError, ValueError):
+        return None
+    return node if node >= 0 else None
+
+
+def host_leg_cpu():
+    """The core the host leg's calling thread runs on, as oneCCL pins each
+    worker to one core (CCL_WORKER_AFFINITY, src/exec/thread/worker.cpp:
+    310-379): the first allowed physical core of the GPU's NUMA node (else
+    of the node core_plan picks), so the buffers it allocates and first
+    touches are local to the GPU's PCIe link; MI_BENCH_HOST_LEG_CPU=c picks
+    core c.  Off by default (MI_BENCH_HOST_LEG_PIN=1 turns it on): on two
+    boxes pinned and unpinned each won the split once (47 against 37 GiB/s
+    and the reverse, profiles/round5_run12/), so the default measures as
+    rounds 1-4 did.  None: unpinned."""
+    if os.environ.get("MI_BENCH_HOST_LEG_PIN", "0") == "0":
+        return None
+    aff = set(os.sched_getaffinity(0))
+    if os.environ.get("MI_BENCH_HOST_LEG_CPU"):
+        c = int(os.environ["MI_BENCH_HOST_LEG_CPU"])
+        return c if c in aff else None
+    node = gpu_numa_node()
+    if node is not None:
+        try:
+            cpus = sorted(set(_cpulist(Path(f"/sys/devices/system/node/node{node}/cpulist").read_text())) & aff)
+        except (OSError, ValueError):
+            cpus = []
+        if cpus:
+            return cpus[0]
+    _, cores, _, _ = core_plan()
+    return cores[0] if cores else None
+
+
 def host_resident_leg(m, dt, es, op, flags, n):
     """The path as oneCCL runs it (host staging buffers in, host result out):
     mi_reduce_sync with pinned and with pageable host buffers.  Reported
-    beside `value`, never as it (PCIe-inclusive rate)."""
+    beside `value`, never as it (PCIe-inclusive rate).  The
+    calling thread is pinned to one core local to the GPU (host_leg_cpu) for
+    the leg, as oneCCL's workers are, and allocates its buffers there."""
+    cpu = host_leg_cpu()
+    prev = os.sched_getaffinity(0)
+    if cpu is not None:
+        os.sched_setaffinity(0, {cpu})
+    try:
+        res = _host_resident_leg(m, dt, es, op, flags, n)
+    finally:
+        os.sched_setaffinity(0, prev)
+    if "error" not in res:
+        res["calling_thread_cpu"] = cpu
+        res["gpu_numa_node"] = gpu_numa_node()
+    return res
+
+
+def _host_resident_leg(m, dt, es, op, flags, n):
     import torch
     res = {}
     nbytes = n * es

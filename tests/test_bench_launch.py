@@ -344,3 +344,21 @@ def test_cpu_sweep_point_pins_and_reduces():
     b, m, r, pin_errors = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
     assert pin_errors == []
     assert b >= m > 0 and r >= 5
+
+
+def test_host_leg_cpu_is_allowed_and_local(monkeypatch):
+    """The host leg's calling thread goes to an allowed core of the GPU's
+    NUMA node (here node 0, or core_plan's node when the GPU's is unknown)
+    under MI_BENCH_HOST_LEG_PIN=1; MI_BENCH_HOST_LEG_PIN=0 (the default)
+    leaves it unpinned."""
+    import os
+    aff = set(os.sched_getaffinity(0))
+    monkeypatch.setenv("MI_BENCH_HOST_LEG_PIN", "1")
+    monkeypatch.setattr(bench, "gpu_numa_node", lambda index=None: 0)
+    c = bench.host_leg_cpu()
+    assert c is None or c in aff
+    monkeypatch.setattr(bench, "gpu_numa_node", lambda index=None: None)
+    c = bench.host_leg_cpu()
+    assert c in aff
+    monkeypatch.setenv("MI_BENCH_HOST_LEG_PIN", "0")
+    assert bench.host_leg_cpu() is None
