@@ -153,7 +153,10 @@ int mi_reduce_batch(const mi_reduce_desc_t* descs, int n, int dtype, int op,
  * Host operands are staged through the GPU in pipelined chunks (H2D, kernel,
  * D2H on a per-thread stream).  `device` < 0 = the calling thread's current
  * HIP device.  Thread-safe: each calling thread has its own stream and
- * scratch (threading contract of src/exec/thread/worker.cpp:310-379).     */
+ * scratch (threading contract of src/exec/thread/worker.cpp:310-379).  A
+ * caller confined to one or two CPUs (a pinned oneCCL worker) has a staged
+ * bucket with pageable operands run by its staging worker, whose CPU set is
+ * the process's, while it waits (MI_REDUCE_CONFINED_HANDOFF=0: inline).   */
 int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype,
                    int op, unsigned flags, int device);
 

@@ -1762,21 +1762,82 @@ int mi_reduce_batch(const mi_reduce_desc_t* descs, int n, int dtype, int op, uns
     return guarded([&]() -> int { return launch_reduce_batch(descs, n, dtype, op, flags, (hipStream_t)stream); });
 }
 
+namespace {
+// A staged bucket from a caller confined to one or two CPUs -- oneCCL pins
+// each worker to one core (CCL_WORKER_AFFINITY, src/exec/thread/worker.cpp:
+// 310-379) -- runs on the thread's staging worker, which has the process's
+// CPU set, while the caller waits.  The runtime pins pageable pages in place
+// on the thread that issues the copy; confined to one core the staged
+// pipeline ran at 17-21 GiB/s of bucket against 24 unconfined
+// (profiles/round5_run12/host_leg_pin_ab.jsonl).  Below the bounce size the
+// CPU copies into pinned buffers on the caller, as before.
+// MI_REDUCE_CONFINED_HANDOFF=0 turns it off.
+bool handoff_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("MI_REDUCE_CONFINED_HANDOFF");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+// some operand is pageable host memory (what the runtime pins in place)
+bool any_pageable(const void* const* inputs, int k, const void* out, size_t bytes) {
+    for (int i = 0; i <= k; i++) {
+        const void* p = i < k ? inputs[i] : out;
+        if (!p) return false;
+        int dev = -1;
+        if (classify(p, &dev, nullptr, bytes) == PK_PAGEABLE) return true;
+    }
+    return false;
+}
+
+bool confined_caller() {
+    if (!handoff_enabled() || !g_helper_cpus.use) return false;
+    cpu_set_t m;
+    CPU_ZERO(&m);
+    if (sched_getaffinity(0, sizeof(m), &m) != 0) return false;
+    const int n = CPU_COUNT(&m);
+    return n <= 2 && CPU_COUNT(&g_helper_cpus.mask) > n;
+}
+
+int sync_entry(const void* const* inputs, int k, void* out, size_t count, int dtype, int op, unsigned flags,
+               int device) {
+    t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
+    const size_t es = dtype_size(dtype);
+    if (es && count * es > kBounceBytes && k >= 1 && k <= MI_MAX_INPUTS && out && confined_caller() &&
+        any_pageable(inputs, k, out, count * es)) {
+        auto j = std::make_shared<AsyncJob>();
+        j->prior = record_prior();
+        for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
+        j->k = k;
+        j->out = out;
+        j->count = count;
+        j->dt = dtype;
+        j->op = op;
+        j->flags = flags;
+        j->device = device;
+        t_stage.submit(j);
+        const int rc = j->wait();
+        return rc ? fail(rc, j->err.c_str()) : 0;
+    }
+    return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+}
+
+}  // namespace
+
 int mi_reduce_sync(const void* in, void* inout, size_t count, int dtype, int op, unsigned flags,
                    int device) {
     return guarded([&]() -> int {
-        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         const void* ins[2] = {inout, in};
-        return reduce_sync(ins, 2, inout, count, dtype, op, flags, device);
+        return sync_entry(ins, 2, inout, count, dtype, op, flags, device);
     });
 }
 
 int mi_reduce_multi_sync(const void* const* inputs, int k, void* out, size_t count, int dtype,
                          int op, unsigned flags, int device) {
     return guarded([&]() -> int {
-        t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
         if (!inputs) return fail(MI_E_INVALID, "null input list");
-        return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
+        return sync_entry(inputs, k, out, count, dtype, op, flags, device);
     });
 }
 

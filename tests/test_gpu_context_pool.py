@@ -73,3 +73,49 @@ def test_concurrent_threads_then_reuse():
     assert not errs, errs[:3]
     # four threads at once take the pooled contexts first
     assert created2 - created1 <= max(0, 4 - pooled1), (created1, pooled1, created2)
+
+
+def test_confined_caller_hands_staged_bucket_to_its_worker():
+    """A caller pinned to one CPU (as oneCCL pins its workers) has its staged
+    pageable buckets run by its staging worker (mi_reduce.hip, sync_entry);
+    the bits are the oracle's, in place and through the K-input entry, and
+    earlier asynchronous requests of the thread still come first."""
+    import os
+    n = (5 << 20) // 4 + 3
+    errs = []
+
+    def body():
+        try:
+            cpu = sorted(os.sched_getaffinity(0))[-1]
+            os.sched_setaffinity(0, {cpu})
+            m = _lib.mi()
+            a = rand_array(FP32, n, seed=901, specials=False)
+            b = rand_array(FP32, n, seed=902, specials=False)
+            c = rand_array(FP32, n, seed=903, specials=False)
+            exp = b.copy()
+            oracle.comp_reduce(a, exp, FP32, 0)
+            # an asynchronous request first (staged: it runs on the worker),
+            # then the synchronous one that reads its output
+            req = ctypes.c_void_p()
+            _lib.check(m.mi_reduce_start(_lib.void_ptr_array([b.ctypes.data, a.ctypes.data]), 2, b.ctypes.data, n,
+                                         FP32, 0, 0, -1, ctypes.byref(req)))
+            exp_c = c.copy()
+            oracle.comp_reduce(exp, exp_c, FP32, 0)
+            _lib.check(m.mi_reduce_sync(b.ctypes.data, c.ctypes.data, n, FP32, 0, 0, -1))
+            _lib.check(m.mi_wait(req))
+            _lib.check(m.mi_request_free(req))
+            assert_same(b, exp, FP32)
+            assert_same(c, exp_c, FP32)
+            out = np.zeros_like(a)
+            exp3 = oracle.fanin([a, b, c], FP32, 0)
+            _lib.check(m.mi_reduce_multi_sync(_lib.void_ptr_array([a.ctypes.data, b.ctypes.data, c.ctypes.data]),
+                                              3, out.ctypes.data, n, FP32, 0, 0, -1))
+            assert_same(out, exp3, FP32)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = threading.Thread(target=body)
+    th.start()
+    th.join()
+    assert wait_os_threads_gone([th.native_id])
+    assert not errs, errs[:3]
