@@ -87,6 +87,11 @@ int mi_ccl_comp_request_free(struct ccl_comp_request* req);
 const char* mi_ccl_reduction_to_str(int op);
 /* Re-read CCL_BF16 / CCL_FP16 / CCL_COMP_HIP_DEVICE (env.cpp:711-720). */
 int mi_ccl_env_reload(void);
+/* The GPU host buckets go to: CCL_COMP_HIP_DEVICE, else the local rank
+ * (MPI_LOCALRANKID / LOCAL_RANK / CCL_LOCAL_RANK, as oneCCL's launchers set
+ * it) modulo the visible GPUs when more than one is visible, else -1 (the
+ * calling thread's current device).  Diagnostic.                          */
+int mi_ccl_comp_device(void);
 /* The calling thread's CPU share of the cooperative split of host buckets
  * above the dispatcher's threshold (pinned = 1: all operands pinned), as
  * adapted by its own split calls; < 0 before the first one.  Diagnostic. */

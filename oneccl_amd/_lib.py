@@ -128,6 +128,7 @@ SHIM_API = [
     ("mi_ccl_comp_pointer_lookups", c_size_t, []),
     ("mi_ccl_comp_shim_sched", c_int, [c_int]),
     ("mi_ccl_impl_types", c_int, [POINTER(c_int), POINTER(c_int)]),
+    ("mi_ccl_comp_device", c_int, []),
     ("mi_ccl_last_error", c_char_p, []),
 ]
 

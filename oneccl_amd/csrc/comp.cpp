@@ -40,6 +40,8 @@
 #include "../../include/mi_host_reduce.h"
 #include "../../include/mi_reduce.h"
 
+static int mi_local_gpu(int local_idx, int ndev);  // below, after the environment
+
 #ifdef MI_ONECCL_TREE
 #include "common/global/global.hpp"
 #include "common/log/log.hpp"
@@ -57,12 +59,14 @@
 #include "mi_ccl_lp_host.hpp"
 static ccl_bf16_impl_type mi_bf16_impl() { return ccl::global_data::env().bf16_impl_type; }
 static ccl_fp16_impl_type mi_fp16_impl() { return ccl::global_data::env().fp16_impl_type; }
-// CCL_COMP_HIP_DEVICE: the GPU for operands that name none (host buffers);
-// read once, like the rest of oneCCL's environment (env.cpp reads it at init).
+// CCL_COMP_HIP_DEVICE: the GPU for operands that name none (host buffers).
+// Unset: the process's index among the node's processes (global_data, set
+// from the launcher at init, global.cpp:96-101,182-220) modulo the GPUs it
+// sees (mi_local_gpu).  Read once, like the rest of oneCCL's environment.
 static int mi_comp_device() {
     static const int dev = [] {
-        const char* v = getenv("CCL_COMP_HIP_DEVICE");
-        return v ? atoi(v) : -1;
+        if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) return atoi(v);
+        return mi_local_gpu(ccl::global_data::get().get_local_proc_idx(), mi_device_count());
     }();
     return dev;
 }
@@ -289,7 +293,19 @@ void parse_env_locked() {
     }
     if (fp16_types.find(e.fp16) == fp16_types.end())
         MI_CCL_THROW("unsupported FP16 impl type: " + fp16_impl_names[e.fp16]);
-    if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) e.device = atoi(v);
+    if (const char* v = getenv("CCL_COMP_HIP_DEVICE")) {
+        e.device = atoi(v);
+    } else {
+        // the launcher's local rank, read as oneCCL's set_local_coord reads
+        // it for hydra, torchrun and no launcher (global.cpp:182-220)
+        int idx = -1;
+        for (const char* name : {"MPI_LOCALRANKID", "LOCAL_RANK", "CCL_LOCAL_RANK"})
+            if (const char* v = getenv(name)) {
+                idx = atoi(v);
+                break;
+            }
+        e.device = mi_local_gpu(idx, mi_device_count());
+    }
     e.host_max = parse_host_max();
     if (const char* v = getenv("CCL_LOG_LEVEL")) e.log_debug = !strcmp(v, "debug") || !strcmp(v, "trace");
     g_env_all.push_back(std::move(snap));
@@ -311,6 +327,12 @@ static int mi_comp_device() { return env().device; }
 static HostMax mi_host_max() { return env().host_max; }
 static bool mi_log_debug_on() { return env().log_debug; }
 #endif  // !MI_ONECCL_TREE
+
+// The GPU for host buckets when the environment names none: the process's
+// local rank modulo the visible GPUs, so the ranks of one node send their
+// host buckets over their own GPUs' PCIe links instead of all over GPU 0's;
+// -1 (the calling thread's current device) for an unknown rank or one GPU.
+static int mi_local_gpu(int local_idx, int ndev) { return local_idx >= 0 && ndev > 1 ? local_idx % ndev : -1; }
 
 // ---------------------------------------------------------------------------
 // semantics selection
@@ -1576,6 +1598,8 @@ double mi_ccl_comp_split_gpu_rate(int pinned, unsigned* gpu_left) {
     if (gpu_left) *gpu_left = t_split.gpu_left[pinned ? 1 : 0];
     return t_split.gpu_rate[pinned ? 1 : 0];
 }
+
+int mi_ccl_comp_device(void) { return mi_comp_device(); }
 
 int mi_ccl_impl_types(int* bf16_impl, int* fp16_impl) {
     MI_SHIM_GUARD({

@@ -214,3 +214,26 @@ def test_context_stats_need_no_device():
     assert _lib.mi().mi_context_stats(ctypes.byref(created), ctypes.byref(pooled)) == 0
     assert created.value >= 0 and pooled.value <= created.value
     assert _lib.mi().mi_context_stats(None, None) == 0
+
+
+def test_host_bucket_device_from_env_and_local_rank(monkeypatch):
+    """CCL_COMP_HIP_DEVICE names the host buckets' GPU; without it the local
+    rank (MPI_LOCALRANKID / LOCAL_RANK / CCL_LOCAL_RANK, as oneCCL's
+    launchers set it) picks one of the visible GPUs, and with at most one
+    visible GPU (none here) the calling thread's current device (-1)."""
+    from oneccl_amd import comp
+    shim = _lib.shim()
+    for k in ("CCL_COMP_HIP_DEVICE", "MPI_LOCALRANKID", "LOCAL_RANK", "CCL_LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    try:
+        monkeypatch.setenv("CCL_COMP_HIP_DEVICE", "3")
+        comp.env_reload()
+        assert shim.mi_ccl_comp_device() == 3
+        monkeypatch.delenv("CCL_COMP_HIP_DEVICE")
+        monkeypatch.setenv("LOCAL_RANK", "5")
+        comp.env_reload()
+        ndev = _lib.mi().mi_device_count()
+        assert shim.mi_ccl_comp_device() == (5 % ndev if ndev > 1 else -1)
+    finally:
+        monkeypatch.undo()
+        comp.env_reload()
