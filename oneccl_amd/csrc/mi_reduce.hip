@@ -1646,6 +1646,24 @@ std::vector<hipEvent_t> record_prior() {
     return evs;
 }
 
+// A staged job for the fold out = inputs[0..k-1] (run by a StageWorker);
+// `ordered`: it first waits for the work this thread already queued on its
+// own streams (record_prior).
+std::shared_ptr<AsyncJob> make_job(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
+                                   unsigned flags, int device, bool ordered) {
+    auto j = std::make_shared<AsyncJob>();
+    if (ordered) j->prior = record_prior();
+    for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
+    j->k = k;
+    j->out = out;
+    j->count = count;
+    j->dt = dt;
+    j->op = op;
+    j->flags = flags;
+    j->device = device;
+    return j;
+}
+
 // Does a fold over these operands need host staging (pageable operands, or
 // pinned ones under MI_HOST_STAGED)?
 bool needs_staging(const void* const* inputs, int k, const void* out, size_t bytes) {
@@ -1806,16 +1824,7 @@ int sync_entry(const void* const* inputs, int k, void* out, size_t count, int dt
     const size_t es = dtype_size(dtype);
     if (es && count * es > kBounceBytes && k >= 1 && k <= MI_MAX_INPUTS && out && confined_caller() &&
         any_pageable(inputs, k, out, count * es)) {
-        auto j = std::make_shared<AsyncJob>();
-        j->prior = record_prior();
-        for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
-        j->k = k;
-        j->out = out;
-        j->count = count;
-        j->dt = dtype;
-        j->op = op;
-        j->flags = flags;
-        j->device = device;
+        auto j = make_job(inputs, k, out, count, dtype, op, flags, device, true);
         t_stage.submit(j);
         const int rc = j->wait();
         return rc ? fail(rc, j->err.c_str()) : 0;
@@ -1956,16 +1965,7 @@ int reduce_start(const void* const* inputs, int k, void* out, size_t count, int 
             // there too, so a thread's requests run in submission order
             // whatever their pointer kinds.
             if (needs_staging(inputs, k, out, count * dtype_size(dtype)) || t_stage.busy()) {
-                auto j = std::make_shared<AsyncJob>();
-                j->prior = record_prior();
-                for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
-                j->k = k;
-                j->out = out;
-                j->count = count;
-                j->dt = dtype;
-                j->op = op;
-                j->flags = flags;
-                j->device = device;
+                auto j = make_job(inputs, k, out, count, dtype, op, flags, device, true);
                 t_stage.submit(j);
                 mi_request* r = new mi_request();
                 r->job = j;
@@ -2056,16 +2056,7 @@ int mi_reduce_split_start(const void* const* inputs, int k, void* out, size_t co
         if (op < MI_OP_SUM || op > MI_OP_MAX)
             return fail(MI_E_INVALID, "unsupported reduction (device path: sum/prod/min/max)");
         t_async_issued = true;
-        auto j = std::make_shared<AsyncJob>();
-        j->prior = record_prior();
-        for (int i = 0; i < k; i++) j->inputs[i] = inputs[i];
-        j->k = k;
-        j->out = out;
-        j->count = count;
-        j->dt = dtype;
-        j->op = op;
-        j->flags = flags;
-        j->device = device;
+        auto j = make_job(inputs, k, out, count, dtype, op, flags, device, true);
         j->head = head_count;
         j->head_fold = head_fold;
         t_stage.submit(j);
@@ -2156,15 +2147,9 @@ int mi_reduce_multi_sync_sharded(const void* const* inputs, int k, void* out, si
         for (int sh = 1; sh < nshards; sh++) {
             const size_t b = std::min(count, per * (size_t)sh), e = std::min(count, b + per);
             if (b >= e) break;
-            auto j = std::make_shared<AsyncJob>();
-            for (int i = 0; i < k; i++) j->inputs[i] = static_cast<const char*>(inputs[i]) + b * es;
-            j->k = k;
-            j->out = static_cast<char*>(out) + b * es;
-            j->count = e - b;
-            j->dt = dtype;
-            j->op = op;
-            j->flags = flags;
-            j->device = devices[sh];
+            const void* sins[MI_MAX_INPUTS];
+            for (int i = 0; i < k; i++) sins[i] = static_cast<const char*>(inputs[i]) + b * es;
+            auto j = make_job(sins, k, static_cast<char*>(out) + b * es, e - b, dtype, op, flags, devices[sh], false);
             jobs.push_back(j);
             try {
                 t_shard_workers[sh - 1]->submit(j);
