@@ -384,11 +384,18 @@ int mi_set_max_blocks(int max_blocks);
  * inherit their creator's mask (MI_REDUCE_HELPER_AFFINITY=inherit).       */
 int mi_helper_cpu_count(void);
 /* Per-thread device contexts (two streams, staging and bounce buffers):
- * *created = contexts built so far, *pooled = contexts of exited threads
- * waiting in the pool for the next thread on their device.  A thread's exit
- * makes no HIP call; its contexts are reused, never freed before the
- * process ends.  Diagnostic.                                               */
+ * *created = contexts that exist (built and not released), *pooled = those
+ * of exited threads, waiting in the pool for the next thread on their
+ * device.  A thread's exit makes no HIP call: its contexts are reused, and
+ * freed only by mi_release_pooled_contexts or the process's end.
+ * Diagnostic.                                                             */
 int mi_context_stats(size_t* created, size_t* pooled);
+/* Free the pooled contexts of exited threads (streams, staging and bounce
+ * buffers: up to 2 x 32 MiB of device memory per host operand slot each).
+ * Work they still hold queued finishes first.  For a point where the
+ * process is done reducing for a while (oneCCL's finalize); the next thread
+ * that needs a context builds a new one.  Returns the number freed.       */
+int mi_release_pooled_contexts(void);
 /* Test hook:a library thread holds an exit guard (the section the exit
  * handler waits for) for hold_ms milliseconds, < 0 = forever.  The handler
  * waits at most MI_REDUCE_EXIT_WAIT_S seconds (default 60), then names the

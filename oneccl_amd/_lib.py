@@ -87,6 +87,7 @@ MI_API = [
     ("mi_set_unaligned_vectors", c_int, [c_int]),
     ("mi_helper_cpu_count", c_int, []),
     ("mi_context_stats", c_int, [POINTER(c_size_t), POINTER(c_size_t)]),
+    ("mi_release_pooled_contexts", c_int, []),
 ]
 
 # mirrors include/mi_ccl_comp.h

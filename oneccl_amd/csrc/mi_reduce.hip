@@ -2552,6 +2552,25 @@ int mi_version(void) { return 100; }  // 0.1.0
 
 int mi_helper_cpu_count(void) { return g_helper_cpus.use ? CPU_COUNT(&g_helper_cpus.mask) : 0; }
 
+int mi_release_pooled_contexts(void) {
+    std::vector<DevCtx*> doomed;
+    {
+        CtxPool& p = ctx_pool();
+        std::lock_guard<std::mutex> lk(p.mu);
+        doomed.swap(p.free);
+    }
+    ExitGuard g("releasing pooled contexts");
+    if (!g.entered) return 0;  // the process is exiting: its teardown frees them
+    for (DevCtx* d : doomed) {
+        for (int s = 0; s < 2; s++)
+            if (d->stream[s]) (void)hipStreamSynchronize(d->stream[s]);
+        if (d->d2h) (void)hipStreamSynchronize(d->d2h);
+        delete d;
+    }
+    g_ctx_created.fetch_sub(doomed.size());
+    return (int)doomed.size();
+}
+
 int mi_context_stats(size_t* created, size_t* pooled) {
     if (created) *created = g_ctx_created.load();
     if (pooled) {

@@ -119,3 +119,26 @@ def test_confined_caller_hands_staged_bucket_to_its_worker():
     th.join()
     assert wait_os_threads_gone([th.native_id])
     assert not errs, errs[:3]
+
+
+def test_release_pooled_contexts():
+    """mi_release_pooled_contexts frees the exited threads' contexts; the
+    next thread builds a fresh one and reduces to the same bits."""
+    n = (3 << 20) // 4 + 7
+    errs = []
+    th = threading.Thread(target=_staged_reduce, args=(700, n, errs))
+    th.start()
+    th.join()
+    assert wait_os_threads_gone([th.native_id])
+    created0, pooled0 = _stats()
+    assert pooled0 >= 1
+    freed = _lib.mi().mi_release_pooled_contexts()
+    created1, pooled1 = _stats()
+    assert freed == pooled0 and pooled1 == 0 and created1 == created0 - freed
+    th = threading.Thread(target=_staged_reduce, args=(702, n, errs))
+    th.start()
+    th.join()
+    assert wait_os_threads_gone([th.native_id])
+    created2, pooled2 = _stats()
+    assert not errs, errs[:3]
+    assert created2 == created1 + 1 and pooled2 == 1
