@@ -481,6 +481,7 @@ def memory_plan(config, layout, world, rank, scaling="weak"):
             ln = lbucket // les
             llay = "tmpbuf" if name == "c4-tmpbuf" else name[len("c2-layout-"):] if name.startswith("c2-") else layout
             legs[name] = input_bytes(lk, ln, les, llay) + parity_bytes(ln, ldt, les, lflags)
+        legs["f3-copy"] = input_bytes(2, GiB // 4, 4, layout) + 9 * PARITY_CHUNK  # ccl_comp_copy on device
         out["config_legs_bytes"] = legs
         peak = max(peak, head + max(legs.values()))
     if world > 1 and config == "c2":
@@ -614,7 +615,7 @@ def timed_steps(step, steps, warmup, stream, world, probe=10):
 CEILING_LIB = "oneccl_amd/lib/libmi_ceiling.so"
 
 
-def measured_ceiling(ins, k, nbytes, stream, launches=10):
+def measured_ceiling(ins, k, nbytes, stream, launches=10, out=None):
     """The achievable ceiling of a k-input reduce on these buffers, in this
     process: the fastest a memory-only kernel reads the k
     input streams (tools/ceiling_probe.hip mic_read_streams: 16-byte
@@ -622,7 +623,8 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
     (mic_write_stream), each over a few launch shapes, best shape taken.
     Reads and writes share HBM, so the reduce's k reads + 1 write cannot
     beat (k + 1) * nbytes / (t_read + t_write).  Writes over ins[0] (the
-    caller refills before its parity check).  None if the probe library is
+    caller refills before its parity check), or over `out` when given (a
+    copy: k = 1, out the destination).  None if the probe library is
     missing (it is measurement infrastructure, not product)."""
     import ctypes
 
@@ -666,13 +668,14 @@ def measured_ceiling(ins, k, nbytes, stream, launches=10):
         return min(res) if res else None
 
     r = best(lambda b, w, fl: L.mic_read_streams(arr, k, nb, b, w, fl, sink.data_ptr(), sh), (0, 1))
-    wr = best(lambda b, w, fl: L.mic_write_stream(ins[0].data_ptr(), nb, b, w, fl, sh), (0, 1, 2))
+    dst = (ins[0] if out is None else out).data_ptr()
+    wr = best(lambda b, w, fl: L.mic_write_stream(dst, nb, b, w, fl, sh), (0, 1, 2))
     # the reads and the write in one launch, in place on ins[0] as the reduce
     # runs (stores ins[0]'s own vectors back: no arithmetic)
     # every residency the LDS granules allow for one-wave blocks (the library
     # picks one of them per k), so the ceiling is not the library's own choice
     mixed_shapes = [(64, w) for w in sorted({waves.value, 5, 8, 9, 11, 16, 21, 25})] + shapes[1:]
-    mx = best(lambda b, w, fl: L.mic_mixed_streams(arr, k, ins[0].data_ptr(), nb, b, w, fl, sh),
+    mx = best(lambda b, w, fl: L.mic_mixed_streams(arr, k, dst, nb, b, w, fl, sh),
               (0, 1, 2), mixed_shapes) if has_mixed else None
     if not r or not wr:
         return None
@@ -798,6 +801,40 @@ def config_legs(m, stream, layout, launches=10):
             legs[name]["ceiling"] = ceil
         del ins, arr
         torch.cuda.empty_cache()
+    # ccl_comp_copy on device (copy_lean_kernel through
+    # mi_copy), 1 GiB from one buffer of the layout to the other
+    ins = alloc_inputs(2, GiB // 4, torch.float32, layout)
+    dst, src = ins[0], ins[1]
+    fill(src, 0xC0C0)
+    for _ in range(2):
+        _lib.check(m.mi_copy(src.data_ptr(), dst.data_ptr(), GiB, 0, sh), "mi_copy")
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(launches):
+        _lib.check(m.mi_copy(src.data_ptr(), dst.data_ptr(), GiB, 0, sh), "mi_copy")
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / launches
+    ceil = measured_ceiling([src], 1, GiB, stream, out=dst)
+    fill(src, 0xC0C1)
+    dst.zero_()
+    _lib.check(m.mi_copy(src.data_ptr(), dst.data_ptr(), GiB, 0, sh), "mi_copy")
+    torch.cuda.synchronize()
+    leg = {"workload": "ccl_comp_copy on device (SURVEY §8(f)3): 1 GiB, mi_copy (copy_lean_kernel)",
+           "layout": LAYOUT_NOTE[layout], "GiBps": round(1.0 / (ms / 1e3), 2), "avg_launch_ms": round(ms, 5),
+           "roofline_frac": round(2 * GiB / (ms / 1e3) / (HBM_PEAK_GBPS * 1e9), 4),
+           "parity": {"elements": src.numel(), "mismatches": count_mismatches(dst, src)}}
+    if ceil:
+        leg["ceiling_TBps"] = ceil["ceiling_TBps"]
+        leg["frac_of_ceiling"] = round(2 * GiB / (ms / 1e3) / 1e12 / ceil["ceiling_TBps"], 4)
+        if "mixed_TBps" in ceil:
+            leg["ceiling_mixed_TBps"] = ceil["mixed_TBps"]
+            leg["frac_of_mixed_ceiling"] = round(2 * GiB / (ms / 1e3) / 1e12 / ceil["mixed_TBps"], 4)
+        leg["ceiling"] = ceil
+    legs["f3-copy"] = leg
+    del ins, dst, src
+    torch.cuda.empty_cache()
     # C1: host buffers through the drop-in entry point
     n = 131072
     rng = np.random.default_rng(0xC1)

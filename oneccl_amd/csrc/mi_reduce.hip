@@ -2204,6 +2204,16 @@ int mi_reduce_sharded(int nshards, const int* devices, const void* const* inputs
     });
 }
 
+// Copies of at least kCopyStreamBytes store with sc1 + nt (each line leaves
+// L2 as it is written, as reduce2_kernel's stores), with no residency cap:
+// one-wave copies of 1 GiB, uncapped, 0.3204 / 0.3168 ms on two boxes
+// against 0.3240 for the library's nt loads + plain stores and 0.3211 with
+// nt stores (box 1); a 25-wave cap won on one box (0.3186) and lost on the
+// other (0.3205), so none (tools/copy_ab.py, profiles/round5_run17/).  Below
+// the threshold the lines a copy writes may be read next from L2 or the
+// MALL, so plain stores (or nt, when the caller asks) stay.
+constexpr size_t kCopyStreamBytes = 64ull << 20;
+
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {
     if (bytes == 0) return 0;
     if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
@@ -2222,7 +2232,9 @@ int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* str
     const uint64_t lean_blocks = (nvec + kCopyBlock - 1) / kCopyBlock;
     if (cap <= 0 && lean_blocks <= 0x7FFFFFFFull) {
         const unsigned blocks = (unsigned)std::max<uint64_t>(lean_blocks, 1);
-        if (nontemporal)
+        if (bytes >= kCopyStreamBytes)  // far past the caches: either flag streams
+            hipLaunchKernelGGL(copy_lean_kernel<5>, dim3(blocks), dim3(kCopyBlock), 0, s, s8, d8, head, nvec, tail);
+        else if (nontemporal)
             hipLaunchKernelGGL(copy_lean_kernel<3>, dim3(blocks), dim3(kCopyBlock), 0, s, s8, d8, head, nvec, tail);
         else
             hipLaunchKernelGGL(copy_lean_kernel<1>, dim3(blocks), dim3(kCopyBlock), 0, s, s8, d8, head, nvec, tail);

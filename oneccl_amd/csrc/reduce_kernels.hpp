@@ -1122,6 +1122,9 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(const char* __restrict__ s
 // copyu / copyconv, profiles/round3_occupancy/).  Round 2's sweep
 // (tools/copy_sweep.hip) had 512 lanes at 6.44 TB/s against 5.78 for
 // copy_kernel<2>, which stays for a capped grid (mi_set_max_blocks).
+// MEM bit 0: nt loads; bit 1: nt stores; bit 2: stores through a per-tile
+// buffer descriptor with sc1 + nt (each line leaves L2 as it is written, as
+// reduce2_kernel stores), for streaming copies far larger than the caches.
 constexpr int kCopyBlock = 64;
 template <int MEM, int B = kCopyBlock>
 __global__ __launch_bounds__(B) void copy_lean_kernel(const char* __restrict__ src8, char* __restrict__ dst8,
@@ -1133,10 +1136,19 @@ __global__ __launch_bounds__(B) void copy_lean_kernel(const char* __restrict__ s
             dst8[o] = src8[o];
         }
     }
-    const uint64_t v = (uint64_t)blockIdx.x * B + threadIdx.x;
-    if (v < nvec)
+    const uint64_t t0 = (uint64_t)blockIdx.x * B;
+    const uint64_t v = t0 + threadIdx.x;
+    if (MEM & 4) {
+        const uint64_t tleft = nvec > t0 ? nvec - t0 : 0;
+        const uint32_t tbytes = (uint32_t)(tleft < (uint64_t)B ? tleft : (uint64_t)B) * 16u;
+        const __amdgpu_buffer_rsrc_t o = tile_rsrc(dst8 + head, t0 * 16, tbytes);
+        if (v < nvec)
+            __builtin_amdgcn_raw_buffer_store_b128(vload<MEM & 1>(reinterpret_cast<const u32x4*>(src8 + head) + v), o,
+                                                   threadIdx.x * 16u, 0, kAuxSC1NT);
+    } else if (v < nvec) {
         vstore<MEM & 2>(reinterpret_cast<u32x4*>(dst8 + head) + v,
                         vload<MEM & 1>(reinterpret_cast<const u32x4*>(src8 + head) + v));
+    }
 }
 
 }  // namespace mi

@@ -288,6 +288,25 @@ def test_comp_copy_any_offsets(nt, cap):
 
 
 @pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("so,do", [(0, 0), (3, 0), (0, 5), (7, 12), (4, 8)])
+def test_comp_copy_streaming_sizes(nt, so, do):
+    """Copies of 64 MiB and more store through per-tile buffer descriptors
+    with sc1 + nt under a residency cap (mi_reduce.hip kCopyStreamBytes):
+    every byte at shifted offsets, nothing written outside the destination,
+    at the threshold, one byte under it and past it with a ragged tail."""
+    import torch
+    base = 64 << 20
+    src = torch.randint(0, 256, (base + 4096,), dtype=torch.uint8, device="cuda")
+    for n in (base - 1, base, base + 1029):
+        dst = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # the fills run on torch's stream, the copy on the library's
+        comp.comp_copy(src.data_ptr() + so, dst.data_ptr() + do, n, bool(nt))
+        assert torch.equal(dst[do:do + n], src[so:so + n]), (so, do, n)
+        assert not dst[:do].any() and not dst[do + n:].any(), (so, do, n)
+        del dst
+
+
+@pytest.mark.parametrize("nt", [0, 1])
 def test_comp_copy(nt):
     import torch
     n = (5 << 20) + 3

@@ -149,6 +149,7 @@ hipError_t launch_mix(dim3 g, dim3 b, unsigned lds, hipStream_t s, const MixArgs
 template <int AUX>
 MixFn pick_mix_k(int k) {
     switch (k) {
+        case 1: return launch_mix<1, AUX>;  // a copy (out != ptrs[0]): ccl_comp_copy's traffic
         case 2: return launch_mix<2, AUX>;
         case 3: return launch_mix<3, AUX>;
         case 4: return launch_mix<4, AUX>;
