@@ -23,7 +23,9 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import bench  # noqa: E402  (kernel_identity: which device code a pass measured)
 
 
-def kernel_values(path: Path, needles=("reduce2_kernel", "reduce_kernel", "fan_kernel")) -> list[float]:
+def kernel_values(path: Path, needles=("mi::reduce2_kernel", "mi::reduce_kernel", "mi::fan_kernel")) -> list[float]:
+    # the library's own namespace: torch's at::native::reduce_kernel (the
+    # parity check's chunked mismatch count) must not be taken for ours
     rows = list(csv.DictReader(open(path)))
     return [float(r["Counter_Value"]) for r in rows if any(n in r["Kernel_Name"] for n in needles)]
 
