@@ -998,7 +998,10 @@ __device__ __forceinline__ void convert_runs(const Pack<typename Tr<ST>::S> (&sp
 }
 
 // 8 elements per lane per group: fp32 side 2 x 16 B, 16-bit side 16 B.
-template <typename ST, typename DT, unsigned V, int B = kBlock>
+// SC1: the vector body's stores go through one buffer descriptor per wave
+// chunk with sc1 + nt (the line leaves L2 as it is written, as reduce2_kernel
+// stores) instead of global nt stores.
+template <typename ST, typename DT, unsigned V, int B = kBlock, bool SC1 = false>
 __global__ __launch_bounds__(B) void convert_kernel(CArgs a) {
     using SS = typename Tr<ST>::S;
     using DS = typename Tr<DT>::S;
@@ -1046,7 +1049,21 @@ __global__ __launch_bounds__(B) void convert_kernel(CArgs a) {
                 for (int v = 0; v < SV; v++) bits |= inf_nan_bits<ST>(__builtin_bit_cast(u32x4, sp[v]));
                 if (__builtin_expect(inf_nan_hit<ST>(bits), 0)) convert_runs<ST, DT, V, true>(sp, dp, ea, eb, a.trunc_from);
             }
-            if constexpr (sizeof(SS) < sizeof(DS)) {
+            if constexpr (SC1) {
+                // the wave chunk's destination: 128 consecutive stores of 16 B
+                // (widening) or 8 B (narrowing), the whole chunk in range
+                constexpr uint32_t SB = sizeof(SS) < sizeof(DS) ? 16u : 8u;
+                const __amdgpu_buffer_rsrc_t o = tile_rsrc(dst, w * 2 * SB, 128u * SB);
+                const uint32_t o0 = (uint32_t)lane * SB, o1 = o0 + 64u * SB;
+                if constexpr (sizeof(SS) < sizeof(DS)) {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dp[0]), o, o0, 0, kAuxSC1NT);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dp[1]), o, o1, 0, kAuxSC1NT);
+                } else {
+                    const u32x4 d = __builtin_bit_cast(u32x4, dp[0]);
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{d.x, d.y}, o, o0, 0, kAuxSC1NT);
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{d.z, d.w}, o, o1, 0, kAuxSC1NT);
+                }
+            } else if constexpr (sizeof(SS) < sizeof(DS)) {
                 vstore<3>(dst + p0, __builtin_bit_cast(u32x4, dp[0]));
                 vstore<3>(dst + p1, __builtin_bit_cast(u32x4, dp[1]));
             } else {

@@ -160,3 +160,31 @@ def test_fp16_vector_entry_points():
 
 def test_unsupported_pair():
     assert _lib.mi().mi_convert(0, 4, 0, 9, 10, 0, None) == -2
+
+
+@pytest.mark.parametrize("ddt,flags,impl", [(BF16, comp.F_BF16_RNE | comp.F_BF16_TAIL_TRUNC16, 2), (BF16, 0, 0),
+                                            (FP16, 0, None)], ids=["bf16rne-tail", "bf16trunc", "fp16"])
+@pytest.mark.parametrize("offs", [(0, 0), (1, 0), (0, 3), (5, 2)])
+def test_streaming_narrowing_conversions(ddt, flags, impl, offs):
+    """Narrowing conversions of 64 MiB of source and more store with sc1 +
+    nt through per-wave buffer descriptors (mi_reduce.hip kConvStreamBytes):
+    the oracle's bits at shifted offsets, a ragged count % 16 tail and
+    nothing written past the destination."""
+    import torch
+    n = (64 << 20) // 4 + 8 * 37 + 13
+    rng = np.random.default_rng(sum(offs) + ddt)
+    src = (rng.standard_normal(n) * 9).astype(np.float32)
+    if ddt == BF16:
+        exp = np.empty(n, np.uint16)
+        oracle.lib().orc_convert_fp32_to_bf16_arrays(src.ctypes.data, exp.ctypes.data, n, impl)
+    else:
+        exp = oracle.f32_to_fp16(src)
+    ts, ps = to_dev(src, offset_elems=offs[0])
+    td = torch.full((n + offs[1] + 64,), 0x5A5A, dtype=torch.int16, device="cuda")
+    pd = td.data_ptr() + 2 * offs[1]
+    torch.cuda.synchronize()
+    _lib.check(_lib.mi().mi_convert(ps, FP32, pd, ddt, n, flags, _stream()))
+    torch.cuda.synchronize()
+    got = td.cpu().numpy().view(np.uint16)
+    assert_same(got[offs[1]:offs[1] + n], exp, ddt)
+    assert (got[:offs[1]] == 0x5A5A).all() and (got[offs[1] + n:] == 0x5A5A).all()

@@ -712,11 +712,12 @@ int main(int argc, char** argv) {
         // conversions: fp32 -> bf16 (RNE) from buf[1] into buf[2]; bf16 -> fp32 back into buf[3]
         const uint64_t count = bytes / 4;
         auto add_conv = [&](auto st, auto dt, auto vconst, auto bconst, int cap, const char* label, const void* src,
-                            void* dst, void* ref, size_t dbytes) {
+                            void* dst, void* ref, size_t dbytes, auto sc1const) {
             using ST = decltype(st);
             using DT = decltype(dt);
             constexpr unsigned V = decltype(vconst)::value;
             constexpr int B = decltype(bconst)::value;
+            constexpr bool SC1 = decltype(sc1const)::value;
             if (cap && cap < B / 64) return;
             const unsigned lds = cap ? lds_for(cap / (B / 64)) : 0;
             CArgs c{};
@@ -727,13 +728,13 @@ int main(int argc, char** argv) {
             c.head = 0;
             c.ngroups = count / 8;
             const uint64_t blocks = std::min<uint64_t>((c.ngroups + B - 1) / B, 1u << 20);
-            const int nb = granted(convert_kernel<ST, DT, V, B>, B, lds);
+            const int nb = granted(convert_kernel<ST, DT, V, B, SC1>, B, lds);
             char name[200];
-            snprintf(name, sizeof name, "%s convert_kernel %dx8, lds %u B/block -> %d blocks = %d waves per CU", label, B,
-                     lds, nb, nb * B / 64);
+            snprintf(name, sizeof name, "%s convert_kernel %dx8%s, lds %u B/block -> %d blocks = %d waves per CU", label,
+                     B, SC1 ? " sc1-nt stores" : "", lds, nb, nb * B / 64);
             vs.push_back({name, label, 6.0 * count, [=](hipStream_t st) {
-                              hipLaunchKernelGGL((convert_kernel<ST, DT, V, B>), dim3((unsigned)blocks), dim3(B), lds, st,
-                                                 c);
+                              hipLaunchKernelGGL((convert_kernel<ST, DT, V, B, SC1>), dim3((unsigned)blocks), dim3(B), lds,
+                                                 st, c);
                               return hipGetLastError();
                           }, dst, ref, dbytes, {}});
         };
@@ -743,10 +744,17 @@ int main(int argc, char** argv) {
         using V0 = std::integral_constant<unsigned, 0u>;
         void* nb16 = buf[2];
         void* nb16b = static_cast<char*>(buf[2]) + bytes / 2;
-        add_conv(float(), bf16_tag(), V2(), I256(), 0, "fp32->bf16 2^28:", buf[1], nb16, nullptr, bytes / 2);
-        for (int cap : {0, 24, 16, 12}) add_conv(float(), bf16_tag(), V2(), I64(), cap, "fp32->bf16 2^28:", buf[1], nb16b, nb16, bytes / 2);
-        add_conv(bf16_tag(), float(), V0(), I256(), 0, "bf16->fp32 2^28:", nb16, buf[3], nullptr, bytes);
-        for (int cap : {0, 24, 16, 12}) add_conv(bf16_tag(), float(), V0(), I64(), cap, "bf16->fp32 2^28:", nb16, buf[4], buf[3], bytes);
+        add_conv(float(), bf16_tag(), V2(), I256(), 0, "fp32->bf16 2^28:", buf[1], nb16, nullptr, bytes / 2, std::false_type());
+        for (int cap : {0, 24, 16, 12}) add_conv(float(), bf16_tag(), V2(), I64(), cap, "fp32->bf16 2^28:", buf[1], nb16b, nb16, bytes / 2, std::false_type());
+        add_conv(bf16_tag(), float(), V0(), I256(), 0, "bf16->fp32 2^28:", nb16, buf[3], nullptr, bytes, std::false_type());
+        for (int cap : {0, 24, 16, 12}) add_conv(bf16_tag(), float(), V0(), I64(), cap, "bf16->fp32 2^28:", nb16, buf[4], buf[3], bytes, std::false_type());
+        // round 5: the same with sc1 + nt stores through per-wave buffer descriptors
+        for (int cap : {0, 24, 16}) {
+            add_conv(float(), bf16_tag(), V2(), I64(), cap, "fp32->bf16 2^28:", buf[1], nb16b, nb16, bytes / 2,
+                     std::true_type());
+            add_conv(bf16_tag(), float(), V0(), I64(), cap, "bf16->fp32 2^28:", nb16, buf[4], buf[3], bytes,
+                     std::true_type());
+        }
     }
     if (which == "fank") {
         // the fan-in at 64-lane blocks over the input count and the wave cap
