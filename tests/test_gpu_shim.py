@@ -923,3 +923,27 @@ def test_registered_pageable_on_gpu_paths(n, dt):
         assert shim.mi_ccl_comp_unregister_host_buffer(ptr(a)) == 0
         assert shim.mi_ccl_comp_unregister_host_buffer(ptr(b)) == 0
     assert_same(b, exp, dt)
+
+
+def test_streaming_copy_and_narrowing_on_pinned_host_memory():
+    """The streaming copy and narrowing conversion (sc1 + nt buffer stores,
+    64 MiB and more) read and write pinned host memory in place as well:
+    device -> pinned, pinned -> device, and fp32 device -> bf16 pinned."""
+    import torch
+    m = _lib.mi()
+    n = (64 << 20) + 4099
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    host = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    back = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(m.mi_copy(src.data_ptr(), host.data_ptr(), n, 0, s))
+    _lib.check(m.mi_copy(host.data_ptr(), back.data_ptr(), n, 1, s))
+    torch.cuda.synchronize()
+    assert torch.equal(host.cuda(), src) and torch.equal(back, src)
+    count = (64 << 20) // 4 + 21
+    f = torch.randn(count, device="cuda") * 5
+    out = torch.zeros(count, dtype=torch.int16).pin_memory()
+    _lib.check(m.mi_convert(f.data_ptr(), FP32, out.data_ptr(), BF16, count, comp.F_BF16_RNE, s))
+    torch.cuda.synchronize()
+    exp = oracle.f32_to_bf16(f.cpu().numpy(), True)
+    assert_same(out.numpy().view(np.uint16), exp, BF16)
