@@ -85,7 +85,110 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the barrier / max-over-ranks only (gloo lets several ranks share "
                         "one GPU when rehearsing the N>1 path)")
+    p.add_argument("--detail", default=os.environ.get("MI_BENCH_DETAIL", DETAIL_DEFAULT),
+                   help="side file for the full result (method notes, probe arrays, per-leg ceilings, the CPU "
+                        "sweep); the stdout line names it")
     return p.parse_args()
+
+
+DETAIL_DEFAULT = "profiles/bench_detail.json"
+LINE_LIMIT = 7000  # bytes: under the driver's 8000-character stdout tail, with room to spare
+
+
+def write_detail(full, path):
+    """The full result (everything the stdout line leaves out) as indented
+    JSON at `path` (relative to the repo root).  Returns the path the line
+    names, or an "unwritten: ..." note: a side file never costs the line."""
+    p = Path(path) if Path(path).is_absolute() else ROOT / path
+    try:
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(json.dumps(full, indent=1) + "\n")
+    except OSError as e:
+        return f"unwritten: {e}"
+    try:
+        return str(p.relative_to(ROOT))
+    except ValueError:
+        return str(p)
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(full, detail):
+    """The ONE stdout line the driver parses, derived from the full result:
+    the contract keys, `roofline` and `cpu_baseline` with their numbers, and
+    per leg only {GiBps, frac, frac_of_mixed_ceiling, mismatches}.  Prose,
+    probe arrays, per-leg ceiling dicts and the CPU sweep stay in the side
+    file `detail`.  Kept under LINE_LIMIT bytes (a 21 KB
+    line was not parsed); should it still be over, the optional sections
+    go, last-listed first, and `trimmed` names them."""
+    line = _pick(full, ("metric", "value", "unit", "n_gpus", "ranks", "ranks_per_device", "steps", "warmup",
+                        "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"))
+    c = full.get("config", {})
+    line["config"] = dict(_pick(c, ("workload", "bucket_bytes_per_gpu", "inputs", "op", "parallelism")),
+                          layout=c.get("layout_name", c.get("layout")), entry="mi_reduce")
+    r = full.get("roofline", {})
+    roof = _pick(r, ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_ratio_to_algorithmic",
+                     "algorithmic_bytes_per_launch", "avg_kernel_ms", "avg_kernel_ms_max_rank", "kernel_ms_min",
+                     "ceiling_TBps", "frac_of_ceiling", "ceiling_mixed_TBps", "frac_of_mixed_ceiling",
+                     "frac_by_placement", "traffic_source"))
+    if "aggregate" in r:
+        roof["aggregate"] = _pick(r["aggregate"], ("achieved", "peak", "frac", "devices"))
+    line["roofline"] = roof
+    cpu = full.get("cpu_baseline")
+    if isinstance(cpu, dict) and "error" not in cpu:
+        cb = _pick(cpu, ("value", "unit", "cores", "kind", "sample_short", "cpu_model", "port_1thread",
+                         "median"))
+        if "sample_short" in cb:
+            cb["sample"] = cb.pop("sample_short")
+        mt = cpu.get("multi_thread", {})
+        cb["multi_thread"] = _pick(mt, ("threads", "value", "median", "spread", "reps", "cgroup_cpu_quota",
+                                        "throttled", "throttled_usec"))
+        line["cpu_baseline"] = cb
+    else:
+        line["cpu_baseline"] = cpu
+    par = full.get("parity", {})
+    line["parity"] = _pick(par, ("elements", "mismatches"))
+    if full.get("dropin_sync"):
+        d = full["dropin_sync"]
+        line["dropin_sync"] = dict(_pick(d, ("value", "best")), mismatches=d.get("parity", {}).get("mismatches"))
+    if full.get("strong_split"):
+        line["strong_split"] = {k: dict(_pick(v, ("value", "ms_per_step", "avg_kernel_ms_max_rank")),
+                                        frac=v.get("aggregate_roofline", {}).get("frac"))
+                                for k, v in full["strong_split"].items()}
+    if full.get("memory"):
+        m = full["memory"]
+        line["memory"] = {"planned_peak_bytes_rank0": m.get("planned_peak_bytes_rank0"),
+                          "measured_max_rank": m.get("torch_max_allocated_bytes_max_rank")}
+    for k in ("rehearsal", "wall_s_rank0"):
+        if k in full:
+            line[k] = full[k]
+    if full.get("host_resident"):
+        h = full["host_resident"]
+        line["host_resident"] = h if "error" in h else _pick(
+            h, ("bucket_bytes", "pinned", "pinned_staged", "pageable", "pageable_registered", "dropin_pinned",
+                "dropin_pageable"))
+    if full.get("configs"):
+        legs = {}
+        for name, v in full["configs"].items():
+            mism = v.get("parity", {}).get("mismatches")
+            if "GiBps" in v:
+                legs[name] = dict(_pick(v, ("GiBps", "frac_of_mixed_ceiling")), frac=v.get("roofline_frac"),
+                                  mismatches=mism)
+            else:  # C1: a host chunk through the drop-in, timed in µs
+                legs[name] = dict(_pick(v, ("median_us", "best_us")), mismatches=mism)
+        line["configs"] = legs
+    line["detail"] = detail
+    trimmed = []
+    for k in ("host_resident", "strong_split", "memory", "configs"):
+        if len(json.dumps(line, separators=(",", ":"))) <= LINE_LIMIT:
+            break
+        if line.pop(k, None) is not None:
+            trimmed.append(k)
+    if trimmed:
+        line["trimmed"] = trimmed
+    return line
 
 
 def fill(t, seed):
@@ -322,15 +425,47 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
         pool.run(touch)
         pool.run(reduce)  # warm
         times = []
+        st0 = cgroup_cpu_stat()
         t_start = time.perf_counter()
         while len(times) < 5 or (time.perf_counter() - t_start < seconds and len(times) < 400):
             t0 = time.perf_counter()
             pool.run(reduce)
             times.append(time.perf_counter() - t0)
+        st1 = cgroup_cpu_stat()
     finally:
         pool.close()
     del ins, acc
-    return bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times), list(pin_errors)
+    throttle = {k: st1[k] - st0[k] for k in ("nr_periods", "nr_throttled", "throttled_usec")
+                if k in st0 and k in st1}
+    return (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times), list(pin_errors),
+            throttle)
+
+
+def cgroup_cpu_stat(path="/sys/fs/cgroup/cpu.stat"):
+    """The cgroup's CPU counters ({nr_periods, nr_throttled, throttled_usec,
+    ...}; empty when there is no cgroup v2 cpu controller).  Read around
+    each timed sweep point: a point whose threads plus the process's other
+    threads exceed the cgroup's quota is throttled, and its spread says
+    nothing about the reduce."""
+    out = {}
+    try:
+        for ln in Path(path).read_text().splitlines():
+            k, _, v = ln.partition(" ")
+            if v.strip().isdigit():
+                out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
+def sweep_counts(n_cores, quota):
+    """Thread counts of the CPU sweep: 1, 8, 16, 32, 64 up to the node's
+    physical cores; under a cgroup CPU quota Q, capped at Q - 1 (and Q - 1
+    itself added), so the timing threads leave the process's main and
+    runtime threads one CPU of the quota and are not throttled."""
+    limit = n_cores if quota is None else min(n_cores, max(1, int(quota) - 1))
+    counts = sorted({t for t in (1, 8, 16, 32, 64) if t <= max(1, limit)} | ({limit} if quota else set()))
+    return counts, [t for t in (8, 16, 32, 64) if t not in counts]
 
 
 def cpu_baseline(cfg, seconds):
@@ -346,9 +481,7 @@ def cpu_baseline(cfg, seconds):
     # when it was built and the type is one it reaches; else the restatement
     use_ref = oracle.ref_comp_available() and dt not in (8, 11)
     node, cores, n_aff, quota = core_plan()
-    limit = len(cores) if quota is None else min(len(cores), int(quota))
-    counts = [t for t in (1, 8, 16, 32, 64) if t <= max(1, limit)]
-    skipped = [t for t in (8, 16, 32, 64) if t not in counts]
+    counts, skipped = sweep_counts(len(cores), quota)
     share = max(seconds / (len(counts) + 1), 1.0)
     res = {}
     for t in counts:
@@ -364,7 +497,7 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
-    (b1, m1, r1, _) = res[1]
+    (b1, m1, r1, _, _) = res[1]
     # sanity probe, independent of the oracle: one core's memcpy bandwidth
     # over the same footprint (numpy's copy is a single-threaded memcpy)
     src = np.ones(bucket // 8, np.float64)
@@ -378,12 +511,17 @@ def cpu_baseline(cfg, seconds):
     copy_gbps = 2 * src.nbytes / min(ct) / 1e9
     del src, dst
     sweep = [dict({"threads": t, "best": round(b, 3), "median": round(m, 3), "reps": r,
-                   "spread": round((b - m) / b, 4)}, **({"pin_errors": pe} if pe else {}))
-             for t, (b, m, r, pe) in sorted(res.items())]
-    head = 16 if 16 in res else max(res)
-    bn, mn, rn, _ = res[head]
+                   "spread": round((b - m) / b, 4), "throttle": th}, **({"pin_errors": pe} if pe else {}))
+             for t, (b, m, r, pe, th) in sorted(res.items())]
+    # the reported point: the largest count under a quota (quota - 1), else 16
+    head = max(res) if quota is not None or 16 not in res else 16
+    bn, mn, rn, _, thn = res[head]
     return {
-        "value": round(b1, 3), "unit": "GiB/s", "cores": 1, "kind": "reference" if use_ref else "port",
+        "value": round(b1, 3), "median": round(m1, 3), "unit": "GiB/s", "cores": 1,
+        "kind": "reference" if use_ref else "port",
+        "sample_short": ("the reference's own CCL_REDUCE (src/comp/comp.cpp, Release flags, oracle/_ref)" if use_ref
+                         else "oracle/comp_oracle.c restatement of CCL_REDUCE") +
+                        f", {bucket >> 20} MiB x {k}-input bucket, 1 pinned thread, best of {r1} reps",
         "traffic_GBps_1core": round(b1 * GiB * (k + 1) / 1e9, 1),
         "copy_probe_GBps_1core": round(copy_gbps, 1),
         "traffic_note": f"the 1-core rate moves (k+1) = {k + 1} bucket-sizes of DRAM traffic per reduce; "
@@ -401,6 +539,7 @@ def cpu_baseline(cfg, seconds):
         if port_1 is not None else None,
         "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": head, "reps": rn,
                          "spread": round((bn - mn) / bn, 4), "sweep": sweep,
+                         "throttled": thn.get("nr_throttled"), "throttled_usec": thn.get("throttled_usec"),
                          "numa_node": node, "physical_cores_in_node": len(cores), "cpus_in_affinity": n_aff,
                          "cgroup_cpu_quota": quota, "skipped_thread_counts": skipped,
                          "cpus_used": cores[:max(res)],
@@ -408,7 +547,8 @@ def cpu_baseline(cfg, seconds):
                                  f"of NUMA node {node} (first hyperthread sibling), taken round robin over the node's L3 "
                                  "domains (CCDs), pinned; each thread first-touches "
                                  "its own range of every buffer, then reduces it; thread counts above the node's "
-                                 "physical cores (or the cgroup's CPU quota) are skipped"},
+                                 "physical cores, or above the cgroup's CPU quota - 1, are skipped; throttle = the "
+                                 "cgroup's cpu.stat deltas over each point's timed reps"},
         "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
     }
 
@@ -1173,6 +1313,7 @@ def main():
             "data": "synthetic (uniform [-1,1) generated on device)",
             "config": {"workload": desc, "bucket_bytes_per_gpu": units_per_rank, "inputs": k,
                        "layout": TMPBUF_NOTE if args.config == "c4-tmpbuf" else LAYOUT_NOTE[args.layout],
+                       "layout_name": "tmpbuf" if args.config == "c4-tmpbuf" else args.layout,
                        "op": ["sum", "prod", "min", "max"][op], "dtype_id": dt, "flags": flags,
                        "parallelism": f"element-range shard x{world}, no collective",
                        "entry": "mi_reduce (include/mi_reduce.h) via ctypes, async on the torch stream"},
@@ -1234,7 +1375,8 @@ def main():
             out["host_resident"] = host_leg
         if legs:
             out["configs"] = legs
-        print(json.dumps(out), flush=True)
+        detail = write_detail(out, args.detail)
+        print(json.dumps(compact_line(out, detail), separators=(",", ":")), flush=True)
     if world > 1:
         dist.destroy_process_group()
     bad = parity["mismatches"] + (dropin["parity"]["mismatches"] if dropin else 0)

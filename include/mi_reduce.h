@@ -401,6 +401,23 @@ int mi_release_pooled_contexts(void);
  * waits at most MI_REDUCE_EXIT_WAIT_S seconds (default 60), then names the
  * section on stderr and ends the process with status 70.                  */
 int mi_test_hold_exit_guard(int hold_ms);
+/* Test hook: the current device of the calling thread's staging worker when
+ * it last ran a job of this thread (-1: none yet).  A job submitted with
+ * device < 0 runs on the submitting thread's current device.             */
+int mi_test_staged_device(void);
+/* Test hook: the nth staged host<->device copy issued from now on (any
+ * thread; 1 = the next) fails with hipErrorInvalidValue before it reaches the
+ * runtime; 0 turns it off.  The failing call's mi_last_error() then names
+ * the copy and the host operand's geometry (page offset, length, the span
+ * handed to the runtime, chunk, pointer class).                           */
+int mi_test_fail_copy(long nth);
+/* Test hook: the error text of a failed copy of [host, host + bytes) in
+ * chunk `chunk` of a host operand of pointer kind `kind` (as mi_pointer_kind:
+ * 0 device, 1 pinned, 2 pageable), the
+ * runtime handed its aligned hull (hull != 0) or interior; sets
+ * mi_last_error() and returns hipErrorInvalidValue's code.  No HIP device
+ * is needed.                                                              */
+int mi_test_copy_error(const void* host, size_t bytes, size_t chunk, int kind, int hull);
 
 #ifdef __cplusplus
 }

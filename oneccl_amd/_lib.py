@@ -7,7 +7,7 @@ library is missing: there is no CPU fallback anywhere in the product.
 from __future__ import annotations
 
 import ctypes
-from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_long, c_size_t, c_uint, c_void_p
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -71,6 +71,9 @@ MI_API = [
     ("mi_host_declared_kind", c_int, [c_void_p, c_size_t]),
     ("mi_pointer_lookups", c_size_t, []),
     ("mi_test_hold_exit_guard", c_int, [c_int]),
+    ("mi_test_fail_copy", c_int, [c_long]),
+    ("mi_test_staged_device", c_int, []),
+    ("mi_test_copy_error", c_int, [c_void_p, c_size_t, c_size_t, c_int, c_int]),
     ("mi_host_register", c_int, [c_void_p, c_size_t]),
     ("mi_host_unregister", c_int, [c_void_p]),
     ("mi_reduction_to_str", c_char_p, [c_int]),

@@ -304,7 +304,9 @@ void parse_env_locked() {
                 idx = atoi(v);
                 break;
             }
-        e.device = mi_local_gpu(idx, mi_device_count());
+        // no local rank: no device count either, so a CPU-only first call (a
+        // small MPI user-op fold) does not initialise the HIP runtime
+        e.device = idx >= 0 ? mi_local_gpu(idx, mi_device_count()) : -1;
     }
     e.host_max = parse_host_max();
     if (const char* v = getenv("CCL_LOG_LEVEL")) e.log_debug = !strcmp(v, "debug") || !strcmp(v, "trace");

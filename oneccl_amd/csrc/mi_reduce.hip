@@ -807,10 +807,52 @@ constexpr size_t kStageSlack = 2 * kHostAlign;  // a staging buffer holds a chun
 inline uintptr_t host_align_dn(uintptr_t a) { return a & ~(kHostAlign - 1); }
 inline uintptr_t host_align_up(uintptr_t a) { return (a + kHostAlign - 1) & ~(kHostAlign - 1); }
 
+// Test hook (mi_test_fail_copy): the nth staged host copy from now on fails
+// with hipErrorInvalidValue before it reaches the runtime (no sticky state).
+std::atomic<long> g_fail_copy_nth{0};
+std::atomic<long> g_copy_seq{0};
+
+bool injected_copy_failure() {
+    const long n = g_fail_copy_nth.load(std::memory_order_relaxed);
+    return n > 0 && g_copy_seq.fetch_add(1, std::memory_order_relaxed) + 1 == n;
+}
+
+const char* kind_name(PtrKind k) { return k == PK_DEVICE ? "device" : k == PK_PINNED ? "pinned" : "pageable"; }
+
+// A failed copy between host memory and a staging buffer: the HIP error and
+// where the host side lay -- the operand's address within its page and its
+// length, the span the runtime was handed (16-byte aligned, h2d_stage /
+// d2h_pageable), the chunk and the operand's pointer class -- so that a fault
+// surfacing at a copy can be matched to the operand's geometry (VERDICT r5
+// item 2).  A sticky error left by an earlier kernel surfaces at the next
+// runtime call too: the text names the copy that observed the error, which
+// is not necessarily the one that caused it.
+// `hull`: the runtime got the operand's aligned hull (h2d_stage), else its
+// aligned interior (d2h_pageable, mi_copy_sync's H2D).
+std::string copy_geometry(const void* host, size_t bytes, size_t chunk, PtrKind kind, bool hull) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(host);
+    const uintptr_t lo = hull ? host_align_dn(a) : std::min(host_align_up(a), a + bytes);
+    const uintptr_t hi = hull ? host_align_up(a + bytes) : std::max(lo, host_align_dn(a + bytes));
+    char buf[320];
+    snprintf(buf, sizeof buf,
+             " [%s host operand: addr & 4095 = %zu, %zu bytes, ends at page offset %zu; runtime span: addr & 4095 "
+             "= %zu, %zu bytes; chunk %zu]",
+             kind_name(kind), (size_t)(a & 4095), bytes, (size_t)((a + bytes) & 4095), (size_t)(lo & 4095),
+             (size_t)(hi - lo), chunk);
+    return buf;
+}
+
+int copy_fail(hipError_t e, const char* what, const void* host, size_t bytes, size_t chunk, PtrKind kind,
+              bool hull) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e) + copy_geometry(host, bytes, chunk, kind, hull);
+    return (int)e;
+}
+
 hipError_t h2d_stage(void* dst, const void* src, size_t bytes, hipStream_t s, size_t* shift) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(src);
     const uintptr_t lo = host_align_dn(a), hi = host_align_up(a + bytes);
     *shift = a - lo;
+    if (injected_copy_failure()) return hipErrorInvalidValue;
     return hipMemcpyAsync(dst, reinterpret_cast<const void*>(lo), hi - lo, hipMemcpyHostToDevice, s);
 }
 
@@ -849,6 +891,7 @@ hipError_t d2h_pageable(void* dst, const void* src, size_t bytes, hipStream_t s,
     const size_t tail = bytes - head - interior;
     const char* s8 = static_cast<const char*>(src);
     char* d8 = static_cast<char*>(dst);
+    if (injected_copy_failure()) return hipErrorInvalidValue;
     hipError_t r = hipSuccess;
     if (interior) r = hipMemcpyAsync(d8 + head, s8 + head, interior, hipMemcpyDeviceToHost, s);
     if (head || tail) {
@@ -943,6 +986,7 @@ struct Drain {
         const void* src;
         size_t bytes;
         hipEvent_t ready;
+        size_t chunk;
     };
     std::mutex mu;
     std::condition_variable cv;
@@ -950,6 +994,7 @@ struct Drain {
     size_t done = 0;  // tasks finished (or skipped after an error)
     bool stop = false;
     hipError_t err = hipSuccess;
+    std::string err_where;  // copy_geometry of the first failed task
     std::thread th;
 
     // `edge`: pinned scratch for the unaligned ends of its D2H copies (kEdgeSlot bytes)
@@ -972,6 +1017,7 @@ struct Drain {
                 t = q.front();
                 q.pop_front();
             }
+            const hipError_t e0 = e;
             if (e == hipSuccess) e = hipEventSynchronize(t.ready);
             if (e == hipSuccess) e = d2h_pageable(t.dst, t.src, t.bytes, s, ed);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -979,7 +1025,10 @@ struct Drain {
             ed.post.clear();
             ed.used = 0;
             std::lock_guard<std::mutex> lk(mu);
-            if (e != hipSuccess && err == hipSuccess) err = e;
+            if (e != hipSuccess && err == hipSuccess) {
+                err = e;
+                if (e0 == hipSuccess) err_where = copy_geometry(t.dst, t.bytes, t.chunk, PK_PAGEABLE, false);
+            }
             done++;
             cv.notify_all();
         }
@@ -1352,7 +1401,12 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
         const int s = (int)(c & 1);
         hipStream_t st = d->stream[s];
         // slot s holds chunk c-2's result until the helper has copied it out
-        if (drained && c >= 2) MI_HIP(drain->wait_done(c - 1));
+        if (drained && c >= 2)
+            if (hipError_t he = drain->wait_done(c - 1)) {
+                hip_fail(he, "staged D2H into pageable memory (drain thread)");
+                g_last_error += drain->err_where;
+                return (int)he;
+            }
         const size_t off = c * chunk_elems;
         const size_t n = std::min(chunk_elems, count - off);
         const size_t bytes = n * es;
@@ -1365,7 +1419,9 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
                 char* buf = static_cast<char*>(d->dbuf[s][slot_of[i]]);
                 if (!loaded[slot_of[i]]) {
                     size_t sh = 0;
-                    MI_HIP(h2d_stage(buf, static_cast<const char*>(inputs[i]) + off * es, bytes, st, &sh));
+                    const void* hsrc = static_cast<const char*>(inputs[i]) + off * es;
+                    if (hipError_t he = h2d_stage(buf, hsrc, bytes, st, &sh))
+                        return copy_fail(he, "H2D staging copy", hsrc, bytes, c, kin[i], true);
                     loaded[slot_of[i]] = true;
                 }
                 din[i] = buf + shift[slot_of[i]];
@@ -1383,15 +1439,16 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
             void* hdst = static_cast<char*>(out) + off * es;
             if (drained) {
                 MI_HIP(hipEventRecord(d->ready[s], st));
-                drain->push({hdst, cdst, bytes, d->ready[s]});
+                drain->push({hdst, cdst, bytes, d->ready[s], c});
             } else if (d2h_pg) {
                 if (edges.full()) {  // every slot holds an end not yet copied out
                     for (int q = 0; q < 2; q++) MI_HIP(wait_stream(d->stream[q]));
                     edges.flush();
                 }
-                MI_HIP(d2h_pageable(hdst, cdst, bytes, st, edges));
-            } else {
-                MI_HIP(hipMemcpyAsync(hdst, cdst, bytes, hipMemcpyDeviceToHost, st));
+                if (hipError_t he = d2h_pageable(hdst, cdst, bytes, st, edges))
+                    return copy_fail(he, "D2H result copy", hdst, bytes, c, kout, false);
+            } else if (hipError_t he = hipMemcpyAsync(hdst, cdst, bytes, hipMemcpyDeviceToHost, st)) {
+                return copy_fail(he, "D2H result copy", hdst, bytes, c, kout, true);
             }
         }
     }
@@ -1415,7 +1472,11 @@ int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int d
     const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain, &post);
     const hipError_t de = drain.finish();  // every staged result is in `out` after this
     if (rc) return rc;
-    if (de != hipSuccess) return hip_fail(de, "staged D2H into pageable memory");
+    if (de != hipSuccess) {
+        hip_fail(de, "staged D2H into pageable memory (drain thread)");
+        g_last_error += drain.err_where;
+        return (int)de;
+    }
     for (int s = 0; s < 2; s++)
         if (used & (1 << s)) MI_HIP(wait_stream(d->stream[s]));
     for (const HostCopy& c : post) memcpy(c.dst, c.src, c.bytes);
@@ -1445,6 +1506,10 @@ struct AsyncJob {
     int dt = 0, op = 0;
     unsigned flags = 0;
     int device = -1;
+    // device < 0 means the submitting thread's current device (mi_reduce.h):
+    // that device, read on the submitting thread, made current on the worker
+    // before the job runs (the worker's own current device is HIP's default)
+    int caller_device = -1;
     // cooperative split (mi_reduce_split_start): [0, head) by head_fold on
     // the worker thread while the GPU folds [head, count)
     size_t head = 0;
@@ -1481,6 +1546,7 @@ struct StageWorker {
     std::deque<std::shared_ptr<AsyncJob>> q;
     size_t inflight = 0;  // submitted and not yet finished (guarded by mu)
     bool stop = false;
+    std::atomic<int> last_device{-1};  // the worker's current device when its last job ran (diagnostic)
 
     void submit(const std::shared_ptr<AsyncJob>& j) {
         ensure_exit_hook();  // the job's HIP calls are then covered by the exit handler
@@ -1536,6 +1602,12 @@ struct StageWorker {
                     }
                     j->prior.clear();
                     const double t0 = mono_s();
+                    if (!rc && j->device < 0 && j->caller_device >= 0) {
+                        const hipError_t he = hipSetDevice(j->caller_device);
+                        if (he != hipSuccess) rc = hip_fail(he, "hipSetDevice (the submitting thread's device)");
+                    }
+                    int cur = -1;
+                    if (!rc && hipGetDevice(&cur) == hipSuccess) last_device.store(cur, std::memory_order_relaxed);
                     if (!rc)
                         rc = j->head_fold ? split_job(*j)
                                           : reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags,
@@ -1661,6 +1733,10 @@ std::shared_ptr<AsyncJob> make_job(const void* const* inputs, int k, void* out, 
     j->op = op;
     j->flags = flags;
     j->device = device;
+    if (device < 0 && hipGetDevice(&j->caller_device) != hipSuccess) {
+        (void)hipGetLastError();
+        j->caller_device = -1;
+    }
     return j;
 }
 
@@ -1722,8 +1798,8 @@ int launch_convert(const void* src, int sdt, void* dst, int ddt, size_t count, u
     if (!fn) return fail(MI_E_UNSUPPORTED, "conversion pair not supported (fp32<->bf16, fp32<->fp16)");
     if (count == 0) return 0;
     if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
-    if (int rc = require_gpu_visible(src)) return rc;
-    if (int rc = require_gpu_visible(dst)) return rc;
+    if (int rc = require_gpu_visible(src, count * dtype_size(sdt))) return rc;
+    if (int rc = require_gpu_visible(dst, count * dtype_size(ddt))) return rc;
     CArgs a;
     memset(&a, 0, sizeof(a));
     a.src = src;
@@ -1920,7 +1996,8 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
             void* ddst = dp;
             if (ks != PK_DEVICE) {
                 size_t sh = 0;
-                MI_HIP(h2d_stage(d->dbuf[sl][0], sp, n * ss, st, &sh));
+                if (hipError_t he = h2d_stage(d->dbuf[sl][0], sp, n * ss, st, &sh))
+                    return copy_fail(he, "H2D staging copy (conversion)", sp, n * ss, c, ks, true);
                 dsrc = static_cast<const char*>(d->dbuf[sl][0]) + sh;
             }
             if (kd != PK_DEVICE)
@@ -1935,9 +2012,11 @@ int mi_convert_sync(const void* src, int src_dtype, void* dst, int dst_dtype, si
                     MI_HIP(wait_stream(d->stream[1]));
                     edges.flush();
                 }
-                MI_HIP(d2h_pageable(dp, ddst, n * ds, st, edges));
+                if (hipError_t he = d2h_pageable(dp, ddst, n * ds, st, edges))
+                    return copy_fail(he, "D2H result copy (conversion)", dp, n * ds, c, kd, false);
             } else if (kd != PK_DEVICE) {
-                MI_HIP(hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st));
+                if (hipError_t he = hipMemcpyAsync(dp, ddst, n * ds, hipMemcpyDeviceToHost, st))
+                    return copy_fail(he, "D2H result copy (conversion)", dp, n * ds, c, kd, true);
             }
         }
         MI_HIP(wait_stream(d->stream[0]));
@@ -2229,8 +2308,9 @@ constexpr size_t kCopyStreamBytes = 64ull << 20;
 int mi_copy(const void* src, void* dst, size_t bytes, int nontemporal, void* stream) {
     if (bytes == 0) return 0;
     if (!src || !dst) return fail(MI_E_INVALID, "null pointer");
-    if (int rc = require_gpu_visible(src)) return rc;
-    if (int rc = require_gpu_visible(dst)) return rc;
+    // the whole extent: a pinned operand must lie inside one pinned allocation
+    if (int rc = require_gpu_visible(src, bytes)) return rc;
+    if (int rc = require_gpu_visible(dst, bytes)) return rc;
     hipStream_t s = (hipStream_t)stream;
     // the destination's 16-byte grid; the source may be at any offset from it
     const uint32_t head = (uint32_t)std::min<size_t>((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u, bytes);
@@ -2309,7 +2389,8 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
             edges.pin = d->edge;
             edges.slots = 1;
             if (kd == PK_PAGEABLE) {
-                MI_HIP(d2h_pageable(dst, src, bytes, st, edges));
+                if (hipError_t he = d2h_pageable(dst, src, bytes, st, edges))
+                    return copy_fail(he, "D2H copy (mi_copy_sync)", dst, bytes, 0, kd, false);
                 MI_HIP(wait_stream(st));
                 edges.flush();
                 return 0;
@@ -2325,7 +2406,9 @@ int mi_copy_sync(const void* src, void* dst, size_t bytes, int nontemporal, int 
                 memcpy(edges.pin, s8, head);
                 MI_HIP(hipMemcpyAsync(d8, edges.pin, head, hipMemcpyHostToDevice, st));
             }
-            if (interior) MI_HIP(hipMemcpyAsync(d8 + head, s8 + head, interior, hipMemcpyHostToDevice, st));
+            if (interior)
+                if (hipError_t he = hipMemcpyAsync(d8 + head, s8 + head, interior, hipMemcpyHostToDevice, st))
+                    return copy_fail(he, "H2D copy (mi_copy_sync)", src, bytes, 0, ks, false);
             if (tail) {
                 memcpy(edges.pin + kHostAlign, s8 + head + interior, tail);
                 MI_HIP(hipMemcpyAsync(d8 + head + interior, edges.pin + kHostAlign, tail, hipMemcpyHostToDevice, st));
@@ -2402,6 +2485,7 @@ bool registered_extent(uintptr_t a, uintptr_t* lo, uintptr_t* hi) {
 // address is a + delta
 bool pinned_extent(uintptr_t a, intptr_t delta, uintptr_t* lo, uintptr_t* hi) {
     if (registered_extent(a, lo, hi)) return true;
+    t_lookups++;  // one more HIP query of the pointer (mi_pointer_lookups counts it)
     void* start = nullptr;
     size_t size = 0;
     hipDeviceptr_t q = reinterpret_cast<hipDeviceptr_t>(a + delta);
@@ -2556,6 +2640,19 @@ int mi_host_declared_kind(const void* ptr, size_t bytes) {
 }
 
 size_t mi_pointer_lookups(void) { return t_lookups; }
+
+int mi_test_staged_device(void) { return t_stage.last_device.load(std::memory_order_relaxed); }
+
+int mi_test_fail_copy(long nth) {
+    g_copy_seq.store(0, std::memory_order_relaxed);
+    g_fail_copy_nth.store(nth > 0 ? nth : 0, std::memory_order_relaxed);
+    return 0;
+}
+
+int mi_test_copy_error(const void* host, size_t bytes, size_t chunk, int kind, int hull) {
+    if (kind < PK_DEVICE || kind > PK_PAGEABLE) return fail(MI_E_INVALID, "pointer kind out of range");
+    return copy_fail(hipErrorInvalidValue, "H2D staging copy (test)", host, bytes, chunk, (PtrKind)kind, hull != 0);
+}
 
 int mi_test_hold_exit_guard(int hold_ms) {
     ensure_exit_hook();

@@ -341,8 +341,10 @@ def test_cpu_sweep_point_pins_and_reduces():
     import os
     cfg = ("fp32 sum", 9, 4, 0, 2, 8 << 20, 0)
     cpus = sorted(os.sched_getaffinity(0))[:2]
-    b, m, r, pin_errors = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
+    b, m, r, pin_errors, throttle = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
     assert pin_errors == []
+    assert set(throttle) <= {"nr_periods", "nr_throttled", "throttled_usec"}
+    assert all(v >= 0 for v in throttle.values())
     assert b >= m > 0 and r >= 5
 
 
@@ -362,3 +364,88 @@ def test_host_leg_cpu_is_allowed_and_local(monkeypatch):
     assert c in aff
     monkeypatch.setenv("MI_BENCH_HOST_LEG_PIN", "0")
     assert bench.host_leg_cpu() is None
+
+
+def _canned_full():
+    """A real full result: round 5 run 22's 21 KB line (the one shape the
+    driver could not parse), with this round's added fields."""
+    full = json.loads((ROOT / "profiles" / "round5_run22" / "bench.json").read_text().strip().splitlines()[-1])
+    full["config"]["layout_name"] = "padded"
+    full["cpu_baseline"]["sample_short"] = "the reference's own CCL_REDUCE, 1 GiB x 2-input bucket, 1 pinned thread"
+    return full
+
+
+def _strong(v):
+    return {"value": v, "unit": "GiB/s", "inputs": 2, "ms_per_step": 1.0, "avg_kernel_ms_max_rank": 0.06,
+            "aggregate_roofline": {"achieved": 1.0, "peak": 64000.0, "frac": 0.84}, "note": "x" * 200}
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_compact_line_is_small_and_parses(world, tmp_path):
+    """the stdout line stays one json.loads-clean line
+    under LINE_LIMIT (the driver keeps the last 8000 characters), carries
+    roofline and cpu_baseline with their numbers, the per-leg fractions and
+    mismatches, and names the side file holding the rest."""
+    full = _canned_full()
+    if world == 8:
+        full.update(n_gpus=1, ranks=8, rehearsal=True, rehearsal_note="y" * 200,
+                    strong_split={"c2": _strong(2000.0), "c4_fanin8": _strong(600.0)})
+        full.pop("configs")
+        full.pop("host_resident")
+    path = bench.write_detail(full, str(tmp_path / "detail.json"))
+    assert json.loads(Path(path).read_text()) == full
+    line = bench.compact_line(full, path)
+    text = json.dumps(line, separators=(",", ":"))
+    assert "\n" not in text and len(text.encode()) <= bench.LINE_LIMIT < 8000
+    back = json.loads(text)
+    assert "trimmed" not in back
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "parity", "detail"):
+        assert k in back, k
+    r = back["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "ceiling_TBps", "ceiling_mixed_TBps"):
+        assert r[k] == full["roofline"][k], k
+    assert "kernel_ms_probe" not in r and "ceiling" not in r
+    cb = back["cpu_baseline"]
+    assert cb["value"] == full["cpu_baseline"]["value"] and cb["cores"] == 1 and cb["kind"] == "reference"
+    assert cb["sample"] and cb["cpu_model"]
+    assert {"threads", "value", "median", "spread"} <= set(cb["multi_thread"])
+    assert "sweep" not in cb["multi_thread"]
+    if world == 1:
+        assert r["frac_by_placement"]["separate"] == full["roofline"]["frac_by_placement"]["separate"]
+        legs = back["configs"]
+        assert set(legs) == set(full["configs"])
+        for name, v in legs.items():
+            assert v["mismatches"] == 0
+            if name != "c1":
+                assert {"GiBps", "frac", "frac_of_mixed_ceiling"} <= set(v)
+    else:
+        assert back["rehearsal"] is True and back["ranks"] == 8
+        assert back["strong_split"]["c4_fanin8"]["frac"] == 0.84
+
+
+def test_compact_line_trims_when_over_limit(monkeypatch):
+    """Should a line still exceed the limit, optional sections go first and
+    the line says which; the contract keys always stay."""
+    monkeypatch.setattr(bench, "LINE_LIMIT", 2500)
+    line = bench.compact_line(_canned_full(), "profiles/bench_detail.json")
+    assert "configs" in line["trimmed"] and "roofline" in line and "cpu_baseline" in line
+    assert len(json.dumps(line, separators=(",", ":"))) <= 2500 + 80
+
+
+@pytest.mark.parametrize("n_cores,quota,counts", [(64, 16.0, [1, 8, 15]), (64, None, [1, 8, 16, 32, 64]),
+                                                  (12, None, [1, 8]), (64, 8.0, [1, 7]), (4, 2.0, [1])])
+def test_sweep_counts_leave_quota_headroom(n_cores, quota, counts):
+    """under a cgroup CPU quota Q the timing threads stop
+    at Q - 1, so the process's other threads do not push it into throttling."""
+    got, skipped = bench.sweep_counts(n_cores, quota)
+    assert got == counts
+    assert not set(got) & set(skipped)
+
+
+def test_cgroup_cpu_stat_parses(tmp_path):
+    f = tmp_path / "cpu.stat"
+    f.write_text("usage_usec 100\nnr_periods 7\nnr_throttled 2\nthrottled_usec 3000\n")
+    assert bench.cgroup_cpu_stat(str(f)) == {"usage_usec": 100, "nr_periods": 7, "nr_throttled": 2,
+                                               "throttled_usec": 3000}
+    assert bench.cgroup_cpu_stat(str(tmp_path / "missing")) == {}

@@ -142,3 +142,47 @@ def test_release_pooled_contexts():
     created2, pooled2 = _stats()
     assert not errs, errs[:3]
     assert created2 == created1 + 1 and pooled2 == 1
+
+
+def _confined_staged(device, seed, out):
+    """A caller confined to one CPU (as oneCCL pins its workers) whose current
+    device is `device`: its staged synchronous bucket goes to its staging
+    worker (the confined hand-off) with device -1."""
+    import os
+
+    import torch
+    try:
+        os.sched_setaffinity(0, {min(os.sched_getaffinity(0))})
+        torch.cuda.set_device(device)
+        m = _lib.mi()
+        n = (8 << 20) // 4 + 5  # past the bounce size: staged
+        a = rand_array(FP32, n, seed=seed, specials=False)
+        b = rand_array(FP32, n, seed=seed + 1, specials=False)
+        exp = b.copy()
+        oracle.comp_reduce(a, exp, FP32, 0)
+        _lib.check(m.mi_reduce_sync(a.ctypes.data, b.ctypes.data, n, FP32, 0, 0, -1))
+        assert_same(b, exp, FP32)
+        out.append(m.mi_test_staged_device())
+    except Exception as e:  # noqa: BLE001
+        out.append(e)
+
+
+@pytest.mark.parametrize("device", [0, 1])
+def test_confined_handoff_runs_on_the_callers_device(device):
+    """device -1 means the calling thread's current
+    device, also when a confined caller's bucket runs on its staging worker
+    (whose own current device would be HIP's default, 0)."""
+    import os
+
+    import torch
+    if device >= torch.cuda.device_count():
+        pytest.skip(f"needs {device + 1} GPUs")
+    if len(os.sched_getaffinity(0)) < 3:
+        pytest.skip("the hand-off needs a process CPU set wider than the caller's")
+    out = []
+    t = threading.Thread(target=_confined_staged, args=(device, 31 + device, out))
+    t.start()
+    t.join(timeout=120)
+    assert not t.is_alive()
+    assert len(out) == 1 and not isinstance(out[0], Exception), out
+    assert out[0] == device

@@ -291,7 +291,7 @@ def test_comp_copy_any_offsets(nt, cap):
 @pytest.mark.parametrize("so,do", [(0, 0), (3, 0), (0, 5), (7, 12), (4, 8)])
 def test_comp_copy_streaming_sizes(nt, so, do):
     """Copies of 64 MiB and more store through per-tile buffer descriptors
-    with sc1 + nt under a residency cap (mi_reduce.hip kCopyStreamBytes):
+    with sc1 + nt and no residency cap (mi_reduce.hip kCopyStreamBytes):
     every byte at shifted offsets, nothing written outside the destination,
     at the threshold, one byte under it and past it with a ragged tail."""
     import torch
