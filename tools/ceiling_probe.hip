@@ -138,7 +138,79 @@ __global__ void mixed_streams(MixArgs a) {
     }
 }
 
+// Other access patterns for the same traffic, no
+// arithmetic, as mixed_streams: each workgroup owns a run of T consecutive
+// tiles (tile = blockDim vectors).  Read phase: every input's vector of each
+// tile, input 0's parked (LDS: in dynamic LDS, T x blockDim x 16 bytes per
+// workgroup; else in registers); write phase: the T tiles stored back to
+// back, a burst of T x blockDim x 16 bytes per workgroup instead of one
+// store per tile between loads.  Each lane stores what it parked itself, so
+// no barrier is needed.  Loads buffer nt, stores STORE_AUX (nt / sc1 nt).
+template <int K, int T, bool LDS, int STORE_AUX>
+__global__ void burst_streams(MixArgs a) {
+    extern __shared__ u32x4 stage[];
+    const uint64_t B = blockDim.x;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * T;
+    u32x4 keep[LDS ? 1 : T];
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const uint64_t v0 = (tile0 + t) * B;
+        if (v0 >= a.nvec) break;
+        const uint64_t left = a.nvec - v0;
+        const uint32_t bytes = (uint32_t)(left < B ? left : B) * 16u;
+        u32x4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            x[j] = __builtin_amdgcn_raw_buffer_load_b128(
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(a.in[j] + v0), (short)0, (int)bytes, 0x00020000),
+                threadIdx.x * 16u, 0, kAuxNT);
+#pragma unroll
+        for (int j = 1; j < K; j++) asm volatile("" ::"v"(x[j]));
+        if constexpr (LDS)
+            stage[t * B + threadIdx.x] = x[0];
+        else
+            keep[t] = x[0];
+    }
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const uint64_t v0 = (tile0 + t) * B;
+        if (v0 >= a.nvec) break;
+        const uint64_t left = a.nvec - v0;
+        const uint32_t bytes = (uint32_t)(left < B ? left : B) * 16u;
+        __builtin_amdgcn_raw_buffer_store_b128(LDS ? stage[t * B + threadIdx.x] : keep[LDS ? 0 : t],
+                                               __builtin_amdgcn_make_buffer_rsrc(a.out + v0, (short)0, (int)bytes,
+                                                                                 0x00020000),
+                                               threadIdx.x * 16u, 0, STORE_AUX);
+    }
+}
+
 typedef hipError_t (*MixFn)(dim3, dim3, unsigned, hipStream_t, const MixArgs&);
+
+template <int K, int T, bool LDS, int AUX>
+hipError_t launch_burst(dim3 g, dim3 b, unsigned lds, hipStream_t s, const MixArgs& a) {
+    hipLaunchKernelGGL((burst_streams<K, T, LDS, AUX>), g, b, lds, s, a);
+    return hipGetLastError();
+}
+
+template <int K, bool LDS, int AUX>
+MixFn pick_burst_t(int t) {
+    switch (t) {
+        case 1: return launch_burst<K, 1, LDS, AUX>;
+        case 2: return launch_burst<K, 2, LDS, AUX>;
+        case 4: return launch_burst<K, 4, LDS, AUX>;
+        case 8: return LDS ? launch_burst<K, 8, true, AUX> : nullptr;
+        case 16: return LDS ? launch_burst<K, 16, true, AUX> : nullptr;
+        case 32: return LDS ? launch_burst<K, 32, true, AUX> : nullptr;
+        default: return nullptr;
+    }
+}
+
+template <int K>
+MixFn pick_burst_k(int t, bool lds, int flavor) {
+    if (flavor == 1) return lds ? pick_burst_t<K, true, kAuxNT>(t) : pick_burst_t<K, false, kAuxNT>(t);
+    if (flavor == 2) return lds ? pick_burst_t<K, true, kAuxSC1NT>(t) : pick_burst_t<K, false, kAuxSC1NT>(t);
+    return nullptr;
+}
 
 template <int K, int AUX>
 hipError_t launch_mix(dim3 g, dim3 b, unsigned lds, hipStream_t s, const MixArgs& a) {
@@ -263,6 +335,31 @@ __attribute__((visibility("default"))) int mic_mixed_streams(const void* const* 
     const uint64_t blocks = (a.nvec + (uint64_t)block - 1) / (uint64_t)block;
     if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
     return (int)fn(dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
+                   static_cast<hipStream_t>(stream), a);
+}
+
+// burst_streams (see above): K reads and one write, each workgroup of
+// `block` threads a run of `tiles` tiles; `lds` 1 parks the outputs in LDS
+// (tiles x block x 16 bytes per workgroup, at most 160 KiB), 0 in registers
+// (tiles <= 4); `waves_per_cu` > 0 adds idle LDS to cap one-wave residency
+// (register mode only); flavor 1 = nt stores, 2 = sc1 nt.  K in {2, 8}.
+__attribute__((visibility("default"))) int mic_burst_streams(const void* const* ptrs, int k, void* out, size_t bytes,
+                                                             int block, int tiles, int lds, int waves_per_cu,
+                                                             int flavor, void* stream) {
+    MixFn fn = k == 2 ? pick_burst_k<2>(tiles, lds != 0, flavor) : k == 8 ? pick_burst_k<8>(tiles, lds != 0, flavor)
+                                                                      : nullptr;
+    if (!fn || !ptrs || !out || bytes % 16 || block < 64 || block > 1024 || block % 64) return -1;
+    const size_t stage = lds ? (size_t)tiles * (size_t)block * 16u : 0;
+    if (stage > 160u * 1024u) return -1;
+    MixArgs a{};
+    for (int j = 0; j < k; j++) a.in[j] = static_cast<const u32x4*>(ptrs[j]);
+    a.out = static_cast<u32x4*>(out);
+    a.nvec = bytes / 16;
+    const uint64_t per = (uint64_t)block * (uint64_t)tiles;
+    const uint64_t blocks = (a.nvec + per - 1) / per;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
+    const unsigned cap = lds ? 0u : lds_for(block, waves_per_cu);
+    return (int)fn(dim3((unsigned)blocks), dim3((unsigned)block), (unsigned)stage > cap ? (unsigned)stage : cap,
                    static_cast<hipStream_t>(stream), a);
 }
 
