@@ -576,6 +576,10 @@ def input_bytes(k, n, es, layout):
 
 
 PARITY_CHUNK = 1 << 24  # elements per mismatch count (count_mismatches)
+# count_nonzero's result and its reduction's scratch beside a chunk's mask:
+# six 512-byte blocks of torch's allocator, measured (the N = 2 and N = 8
+# rehearsals' peaks, profiles/round5_run10/, profiles/round6_run2/)
+PARITY_COUNT_SMALL = 3072
 
 
 def parity_bytes(n, dt, es, flags=0):
@@ -584,13 +588,14 @@ def parity_bytes(n, dt, es, flags=0):
     one widened input, then the rounding: an int32 shift and the storage copy
     for bf16 truncation, the storage copy otherwise), then the expected result
     beside one chunk's mismatch mask and its int64 count (9 bytes per element
-    of a chunk).  Measured equal with MI_BENCH_MEM_TRACE=1."""
+    of a chunk, plus the count's few small blocks).  Measured equal with
+    MI_BENCH_MEM_TRACE=1."""
     if dt in (8, 11):
         trunc = dt == 11 and not (flags & 0x2)
         fold = max(8 * n, (4 + 4 + es) * n if trunc else (4 + es) * n)
     else:
         fold = es * n
-    return max(fold, es * n + 9 * min(n, PARITY_CHUNK))
+    return max(fold, es * n + 9 * min(n, PARITY_CHUNK) + PARITY_COUNT_SMALL)
 
 
 def memory_plan(config, layout, world, rank, scaling="weak"):

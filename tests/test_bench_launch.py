@@ -295,7 +295,10 @@ def test_memory_plan_layouts_and_tmpbuf():
     assert p["parity_temporaries_bytes"] == (128 << 20) * (4 + 4)
     assert bench.parity_bytes(128 << 20, 11, 2, 0) == (128 << 20) * (4 + 4 + 2)  # truncation: int32 shift too
     p = bench.memory_plan("c2", "padded", 1, 0)  # the accumulator; then result + one chunk's mask and count
-    assert p["parity_temporaries_bytes"] == GIB + 9 * bench.PARITY_CHUNK
+    assert p["parity_temporaries_bytes"] == GIB + 9 * bench.PARITY_CHUNK + bench.PARITY_COUNT_SMALL
+    # the rehearsals' measured per-rank peaks (N = 2 and N = 8: head + parity)
+    for world in (2, 8):
+        assert bench.memory_plan("c2", "padded", world, 0)["peak_bytes"] == 4311747584
 
 
 @pytest.mark.parametrize("dt,flags", [(9, 0), (4, 0), (6, 0), (11, 0), (11, 0x2), (11, 0x6), (8, 0), (8, 0x4)])

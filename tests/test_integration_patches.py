@@ -17,6 +17,7 @@ reference tree is only read.  Runs where /root/reference exists.
   0004  allreduce.cpp nreduce + entry_factory.hpp: one fused fan-in per segment (§2e)
   0005  buffer_cache.cpp: the regular buffer cache declares its host buffers     (§2h)
   0006  copy_entry.cpp, recv_copy_entry.cpp: host copies say so (no lookup)      (§2i)
+  0007  global.cpp: finalize frees libmi_reduce's pooled per-thread contexts     (§2j)
 """
 from __future__ import annotations
 
@@ -45,6 +46,7 @@ UNITS = {  # translation units the patches touch (headers through their includer
     "buffer_cache": "src/sched/buffer/buffer_cache.cpp",
     "copy_entry": "src/sched/entry/copy/copy_entry.cpp",
     "recv_copy_entry": "src/sched/entry/recv_copy_entry.cpp",
+    "global": "src/common/global/global.cpp",
 }
 
 
@@ -91,7 +93,8 @@ def test_patch_set_is_complete():
     names = [p.name for p in PATCHES]
     assert names == ["0001-build-swap-src-comp.patch", "0002-atl-mpi-fp16-user-op.patch",
                      "0003-async-host-reduce-entries.patch", "0004-nreduce-fused-fanin.patch",
-                     "0005-buffer-cache-declares-host-buffers.patch", "0006-copy-entries-host-copy.patch"], names
+                     "0005-buffer-cache-declares-host-buffers.patch", "0006-copy-entries-host-copy.patch",
+                     "0007-finalize-releases-pooled-contexts.patch"], names
     assert (NEW_FILES / "sched" / "entry" / "batch_reduce_entry.hpp").exists()
 
 
@@ -165,3 +168,18 @@ def test_buffer_cache_declares_exactly_what_it_frees(tree, objs):
     need = _undefs(objs["buffer_cache"][0])
     assert {"mi_ccl_comp_register_host_buffer", "mi_ccl_comp_unregister_host_buffer"} <= need
     assert {"mi_ccl_comp_register_host_buffer", "mi_ccl_comp_unregister_host_buffer"} <= _global_defs(objs["ours"][0])
+
+
+def test_finalize_releases_pooled_contexts(tree, objs):
+    """0007: oneCCL's global reset frees the contexts of the
+    exited workers (streams, staging and bounce buffers) once the executor
+    has joined them; the call is libmi_reduce's C export."""
+    import ctypes
+    d, _ = tree
+    src = (d / "src" / "common" / "global" / "global.cpp").read_text()
+    body = src[src.index("ccl::status global_data::reset()"):]
+    assert body.index("executor.reset();") < body.index("mi_release_pooled_contexts();")
+    assert "mi_release_pooled_contexts" in _undefs(objs["global"][0])
+    lib = ROOT / "oneccl_amd" / "lib" / "libmi_reduce.so"
+    if lib.exists():
+        assert hasattr(ctypes.CDLL(str(lib)), "mi_release_pooled_contexts")
