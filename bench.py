@@ -1166,6 +1166,10 @@ def main():
         else:
             dist.init_process_group("gloo")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    # a gloo group for the ranks that wait while rank 0 times the host cores:
+    # they block in a socket read, where an RCCL barrier's stream wait could
+    # poll on the CPUs the baseline is measuring
+    idle_pg = dist.new_group(backend="gloo") if world > 1 and args.dist_backend == "nccl" else None
     pg_world = dist.get_world_size() if world > 1 else 1  # the ranks the process group saw
     ident = device_identity(torch.cuda.current_device())
     idents = [ident]
@@ -1268,7 +1272,9 @@ def main():
             log(f"cpu_baseline failed: {cpu['error']}")
         if world > 1 and "error" not in cpu:
             cpu["note_n_gpus"] = (f"measured on rank 0 after the {world}-rank timed region and a barrier, while the "
-                                  "other ranks idle; the same bounded sample as at N=1")
+                                  "other ranks wait in a gloo barrier; the same bounded sample as at N=1")
+    if world > 1:
+        dist.barrier(group=idle_pg)  # the other ranks wait here, off the CPUs, until rank 0 is done
 
     legs = None
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_config_legs:
