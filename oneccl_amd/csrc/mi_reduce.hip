@@ -1250,6 +1250,33 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
     return 0;
 }
 
+// Every operand's kind, device-visible address and device, classified once
+// (sync_entry, for a confined caller's hand-off) and handed to reduce_issue,
+// which would otherwise classify them again (three
+// classifications per bucket for a pinned oneCCL worker, now two).
+struct Kinds {
+    bool valid = false;
+    PtrKind kin[MI_MAX_INPUTS];
+    const void* dins[MI_MAX_INPUTS];
+    int dev_in[MI_MAX_INPUTS];
+    PtrKind kout = PK_PAGEABLE;
+    void* dout = nullptr;
+    int dev_out = -1;
+};
+
+void classify_all(const void* const* inputs, int k, void* out, size_t bytes, Kinds* c) {
+    for (int i = 0; i < k; i++) {
+        void* dp = const_cast<void*>(inputs[i]);
+        c->dev_in[i] = -1;
+        c->kin[i] = classify(inputs[i], &c->dev_in[i], &dp, bytes);
+        c->dins[i] = dp;
+    }
+    c->dout = out;
+    c->dev_out = -1;
+    c->kout = classify(out, &c->dev_out, &c->dout, bytes);
+    c->valid = true;
+}
+
 // Issue a fold with any pointer kinds on the calling thread's streams of the
 // chosen device; *used = the streams that carry work (bit 0: stream[0],
 // bit 1: stream[1]).  All-device or zero-copy: one launch on stream[0].
@@ -1257,7 +1284,8 @@ int ensure_scratch(DevCtx* d, size_t nbuf, size_t bytes) {
 // of chunk c+1 overlaps the kernel / D2H of chunk c).
 int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
                  unsigned flags, int device, DevCtx** ctx, int* used, Drain* drain = nullptr,
-                 std::vector<HostCopy>* post = nullptr, hipEvent_t* t_start = nullptr) {
+                 std::vector<HostCopy>* post = nullptr, hipEvent_t* t_start = nullptr,
+                 const Kinds* pre = nullptr) {
     *ctx = nullptr;
     *used = 0;
     const size_t es = dtype_size(dt);
@@ -1268,24 +1296,26 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
     for (int i = 0; i < k; i++)
         if (!inputs[i]) return fail(MI_E_INVALID, "null input");
 
-    PtrKind kin[MI_MAX_INPUTS];
-    const void* dins[MI_MAX_INPUTS];
+    Kinds own;
+    if (!pre || !pre->valid) {
+        classify_all(inputs, k, out, count * es, &own);
+        pre = &own;
+    }
+    const PtrKind* kin = pre->kin;
+    const void* const* dins = pre->dins;
     int pdev = -1;
     bool all_dev = true, mixed_dev = false;
     for (int i = 0; i < k; i++) {
-        void* dp = const_cast<void*>(inputs[i]);
-        int d_i = -1;
-        kin[i] = classify(inputs[i], &d_i, &dp, count * es);
-        dins[i] = dp;
+        const int d_i = pre->dev_in[i];
         all_dev = all_dev && kin[i] == PK_DEVICE;
         if (d_i >= 0) {
             mixed_dev = mixed_dev || (pdev >= 0 && d_i != pdev);
             pdev = d_i;
         }
     }
-    void* dout = out;
-    int d_o = -1;
-    const PtrKind kout = classify(out, &d_o, &dout, count * es);
+    void* dout = pre->dout;
+    const int d_o = pre->dev_out;
+    const PtrKind kout = pre->kout;
     all_dev = all_dev && kout == PK_DEVICE;
     if (d_o >= 0) {
         mixed_dev = mixed_dev || (pdev >= 0 && d_o != pdev);
@@ -1464,12 +1494,13 @@ int reduce_issue(const void* const* inputs, int k, void* out, size_t count, int 
 }
 
 int reduce_sync(const void* const* inputs, int k, void* out, size_t count, int dt, int op,
-                unsigned flags, int device) {
+                unsigned flags, int device, const Kinds* pre = nullptr) {
     DevCtx* d = nullptr;
     int used = 0;
     Drain drain;
     std::vector<HostCopy> post;
-    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain, &post);
+    const int rc = reduce_issue(inputs, k, out, count, dt, op, flags, device, &d, &used, &drain, &post, nullptr,
+                                pre);
     const hipError_t de = drain.finish();  // every staged result is in `out` after this
     if (rc) return rc;
     if (de != hipSuccess) {
@@ -1506,6 +1537,7 @@ struct AsyncJob {
     int dt = 0, op = 0;
     unsigned flags = 0;
     int device = -1;
+    Kinds kinds;  // the operands as the submitting thread classified them (valid: use them)
     // device < 0 means the submitting thread's current device (mi_reduce.h):
     // that device, read on the submitting thread, made current on the worker
     // before the job runs (the worker's own current device is HIP's default)
@@ -1611,7 +1643,7 @@ struct StageWorker {
                     if (!rc)
                         rc = j->head_fold ? split_job(*j)
                                           : reduce_sync(j->inputs, j->k, j->out, j->count, j->dt, j->op, j->flags,
-                                                        j->device);
+                                                        j->device, &j->kinds);
                     j->t_run = mono_s() - t0;  // published by the done flag below
                 }
             }
@@ -1887,13 +1919,10 @@ bool handoff_enabled() {
 }
 
 // some operand is pageable host memory (what the runtime pins in place)
-bool any_pageable(const void* const* inputs, int k, const void* out, size_t bytes) {
-    for (int i = 0; i <= k; i++) {
-        const void* p = i < k ? inputs[i] : out;
-        if (!p) return false;
-        int dev = -1;
-        if (classify(p, &dev, nullptr, bytes) == PK_PAGEABLE) return true;
-    }
+bool any_pageable(const Kinds& c, int k) {
+    if (c.kout == PK_PAGEABLE) return true;
+    for (int i = 0; i < k; i++)
+        if (c.kin[i] == PK_PAGEABLE) return true;
     return false;
 }
 
@@ -1910,12 +1939,20 @@ int sync_entry(const void* const* inputs, int k, void* out, size_t count, int dt
                int device) {
     t_stage.wait_idle();  // this thread's earlier asynchronous requests come first
     const size_t es = dtype_size(dtype);
-    if (es && count * es > kBounceBytes && k >= 1 && k <= MI_MAX_INPUTS && out && confined_caller() &&
-        any_pageable(inputs, k, out, count * es)) {
-        auto j = make_job(inputs, k, out, count, dtype, op, flags, device, true);
-        t_stage.submit(j);
-        const int rc = j->wait();
-        return rc ? fail(rc, j->err.c_str()) : 0;
+    if (es && count * es > kBounceBytes && k >= 1 && k <= MI_MAX_INPUTS && out && confined_caller()) {
+        bool nonnull = true;
+        for (int i = 0; i < k; i++) nonnull = nonnull && inputs[i];
+        if (nonnull) {
+            // classified once here; the staging worker (or this thread) reuses it
+            Kinds c;
+            classify_all(inputs, k, out, count * es, &c);
+            if (!any_pageable(c, k)) return reduce_sync(inputs, k, out, count, dtype, op, flags, device, &c);
+            auto j = make_job(inputs, k, out, count, dtype, op, flags, device, true);
+            j->kinds = c;
+            t_stage.submit(j);
+            const int rc = j->wait();
+            return rc ? fail(rc, j->err.c_str()) : 0;
+        }
     }
     return reduce_sync(inputs, k, out, count, dtype, op, flags, device);
 }

@@ -186,3 +186,44 @@ def test_confined_handoff_runs_on_the_callers_device(device):
     assert not t.is_alive()
     assert len(out) == 1 and not isinstance(out[0], Exception), out
     assert out[0] == device
+
+
+@pytest.mark.parametrize("confined", [False, True])
+def test_sync_bucket_classifies_each_operand_once(confined):
+    """a synchronous bucket classifies each operand once,
+    also on the confined caller's path (which used to classify them again
+    before reduce_issue did).  Pinned, undeclared operands: one HIP lookup
+    for the kind and one for the pinned allocation's extent (counted since
+    round 6) per operand; in place, `out` is the first input's pointer."""
+    import os
+
+    import torch
+    if confined and len(os.sched_getaffinity(0)) < 3:
+        pytest.skip("the hand-off needs a process CPU set wider than the caller's")
+    res = []
+
+    def body():
+        try:
+            if confined:
+                os.sched_setaffinity(0, {min(os.sched_getaffinity(0))})
+            m = _lib.mi()
+            n = (4 << 20) // 4 + 3
+            a = rand_array(FP32, n, seed=41, specials=False)
+            b = rand_array(FP32, n, seed=42, specials=False)
+            exp = b.copy()
+            oracle.comp_reduce(a, exp, FP32, 0)
+            ha = torch.from_numpy(a.view(np.uint8).copy()).pin_memory()
+            hb = torch.from_numpy(b.view(np.uint8).copy()).pin_memory()
+            n0 = m.mi_pointer_lookups()
+            _lib.check(m.mi_reduce_sync(ha.data_ptr(), hb.data_ptr(), n, FP32, 0, 0, -1))
+            res.append(m.mi_pointer_lookups() - n0)
+            assert_same(hb.numpy().view(np.float32), exp, FP32)
+        except Exception as e:  # noqa: BLE001
+            res.append(e)
+
+    t = threading.Thread(target=body)
+    t.start()
+    t.join(timeout=120)
+    assert not t.is_alive()
+    assert res and not isinstance(res[-1], Exception), res
+    assert res[0] == 2 * 3, res
