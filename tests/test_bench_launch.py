@@ -452,3 +452,15 @@ def test_cgroup_cpu_stat_parses(tmp_path):
     assert bench.cgroup_cpu_stat(str(f)) == {"usage_usec": 100, "nr_periods": 7, "nr_throttled": 2,
                                                "throttled_usec": 3000}
     assert bench.cgroup_cpu_stat(str(tmp_path / "missing")) == {}
+
+
+def test_compact_line_of_a_real_8_rank_rehearsal():
+    """The full result the 8-rank rehearsal wrote as its side file
+    (profiles/round6_run2/) gives back the line it printed."""
+    full = json.loads((ROOT / "profiles" / "round6_run2" / "bench_gpus8_detail.json").read_text())
+    printed = json.loads((ROOT / "profiles" / "round6_run2" / "bench_gpus8_rehearsal.json").read_text()
+                         .strip().splitlines()[-1])
+    line = bench.compact_line(full, printed["detail"])
+    assert line == printed
+    assert len(json.dumps(line, separators=(",", ":"))) <= bench.LINE_LIMIT
+    assert line["rehearsal"] is True and line["ranks"] == 8 and line["parity"]["mismatches"] == 0
