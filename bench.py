@@ -144,7 +144,7 @@ def compact_line(full, detail):
             cb["sample"] = cb.pop("sample_short")
         mt = cpu.get("multi_thread", {})
         cb["multi_thread"] = _pick(mt, ("threads", "value", "median", "spread", "reps", "cgroup_cpu_quota",
-                                        "throttled", "throttled_usec"))
+                                        "throttled", "throttled_usec", "psi_cpu_some_us"))
         line["cpu_baseline"] = cb
     else:
         line["cpu_baseline"] = cpu
@@ -425,18 +425,21 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
         pool.run(touch)
         pool.run(reduce)  # warm
         times = []
-        st0 = cgroup_cpu_stat()
+        st0, ps0 = cgroup_cpu_stat(), psi_totals()
         t_start = time.perf_counter()
         while len(times) < 5 or (time.perf_counter() - t_start < seconds and len(times) < 400):
             t0 = time.perf_counter()
             pool.run(reduce)
             times.append(time.perf_counter() - t0)
-        st1 = cgroup_cpu_stat()
+        st1, ps1 = cgroup_cpu_stat(), psi_totals()
     finally:
         pool.close()
     del ins, acc
     throttle = {k: st1[k] - st0[k] for k in ("nr_periods", "nr_throttled", "throttled_usec")
                 if k in st0 and k in st1}
+    # tasks of this machine (or VM) waiting for a CPU / stalled on memory
+    # during the timed reps, in microseconds (/proc/pressure, "some")
+    throttle.update({f"psi_{k}_some_us": ps1[k] - ps0[k] for k in ps0 if k in ps1})
     return (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times), list(pin_errors),
             throttle)
 
@@ -455,6 +458,20 @@ def cgroup_cpu_stat(path="/sys/fs/cgroup/cpu.stat"):
                 out[k] = int(v)
     except OSError:
         pass
+    return out
+
+
+def psi_totals(root="/proc/pressure"):
+    """Pressure-stall totals ({"cpu": us, "memory": us}, the "some" line;
+    empty where the kernel has no PSI)."""
+    out = {}
+    for k in ("cpu", "memory"):
+        try:
+            for ln in Path(root, k).read_text().splitlines():
+                if ln.startswith("some"):
+                    out[k] = int(ln.rsplit("total=", 1)[1])
+        except (OSError, ValueError, IndexError):
+            pass
     return out
 
 
@@ -540,6 +557,7 @@ def cpu_baseline(cfg, seconds):
         "multi_thread": {"value": round(bn, 3), "median": round(mn, 3), "threads": head, "reps": rn,
                          "spread": round((bn - mn) / bn, 4), "sweep": sweep,
                          "throttled": thn.get("nr_throttled"), "throttled_usec": thn.get("throttled_usec"),
+                         "psi_cpu_some_us": thn.get("psi_cpu_some_us"),
                          "numa_node": node, "physical_cores_in_node": len(cores), "cpus_in_affinity": n_aff,
                          "cgroup_cpu_quota": quota, "skipped_thread_counts": skipped,
                          "cpus_used": cores[:max(res)],

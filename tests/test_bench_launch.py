@@ -346,7 +346,8 @@ def test_cpu_sweep_point_pins_and_reduces():
     cpus = sorted(os.sched_getaffinity(0))[:2]
     b, m, r, pin_errors, throttle = bench.cpu_sweep_point(cfg, cpus, 0.2, False)
     assert pin_errors == []
-    assert set(throttle) <= {"nr_periods", "nr_throttled", "throttled_usec"}
+    assert set(throttle) <= {"nr_periods", "nr_throttled", "throttled_usec", "psi_cpu_some_us",
+                             "psi_memory_some_us"}
     assert all(v >= 0 for v in throttle.values())
     assert b >= m > 0 and r >= 5
 
@@ -464,3 +465,11 @@ def test_compact_line_of_a_real_8_rank_rehearsal():
     assert line == printed
     assert len(json.dumps(line, separators=(",", ":"))) <= bench.LINE_LIMIT
     assert line["rehearsal"] is True and line["ranks"] == 8 and line["parity"]["mismatches"] == 0
+
+
+def test_psi_totals_parse(tmp_path):
+    (tmp_path / "cpu").write_text("some avg10=0.45 avg60=0.40 avg300=0.17 total=193073552\n"
+                                  "full avg10=0.00 avg60=0.00 avg300=0.00 total=0\n")
+    (tmp_path / "memory").write_text("some avg10=0.00 avg60=0.00 avg300=0.00 total=12\n")
+    assert bench.psi_totals(str(tmp_path)) == {"cpu": 193073552, "memory": 12}
+    assert bench.psi_totals(str(tmp_path / "none")) == {}
