@@ -1127,6 +1127,24 @@ def launch_ranks(plans, timeout=None):
     return failed if failed >= 0 else 128 - failed  # killed by signal s -> 128 + s
 
 
+class stdout_to_stderr:
+    """File descriptor 1 points at stderr inside the block: native libraries
+    (gloo prints its rendezvous notes with printf) cannot put lines before
+    the one JSON line the driver parses."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def device_identity(index):
     """A physical device's identity: PCI domain:bus:device and UUID (ranks on
     one GPU share it).  Should the runtime report neither, the identity falls
@@ -1179,15 +1197,19 @@ def main():
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(local_rank % max(ndev, 1))
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo")
+        with stdout_to_stderr():  # gloo's "connected to N peer ranks" notes: stdout carries the line only
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group("gloo")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     # a gloo group for the ranks that wait while rank 0 times the host cores:
     # they block in a socket read, where an RCCL barrier's stream wait could
     # poll on the CPUs the baseline is measuring
-    idle_pg = dist.new_group(backend="gloo") if world > 1 and args.dist_backend == "nccl" else None
+    idle_pg = None
+    if world > 1 and args.dist_backend == "nccl":
+        with stdout_to_stderr():
+            idle_pg = dist.new_group(backend="gloo")
     pg_world = dist.get_world_size() if world > 1 else 1  # the ranks the process group saw
     ident = device_identity(torch.cuda.current_device())
     idents = [ident]

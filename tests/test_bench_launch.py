@@ -473,3 +473,38 @@ def test_psi_totals_parse(tmp_path):
     (tmp_path / "memory").write_text("some avg10=0.00 avg60=0.00 avg300=0.00 total=12\n")
     assert bench.psi_totals(str(tmp_path)) == {"cpu": 193073552, "memory": 12}
     assert bench.psi_totals(str(tmp_path / "none")) == {}
+
+
+def test_stdout_to_stderr_moves_native_writes(capfd):
+    """Writes to file descriptor 1 inside the block (as gloo's printf) land
+    on stderr; stdout keeps only what is written outside it."""
+    print("before", flush=True)
+    with bench.stdout_to_stderr():
+        os.write(1, b"native note\n")
+    print("after", flush=True)
+    out, err = capfd.readouterr()
+    assert out == "before\nafter\n" and "native note" in err
+
+
+def test_gloo_group_notes_stay_off_stdout():
+    """Two gloo ranks created under stdout_to_stderr print nothing on stdout
+    but what the script prints (the rank-0 line)."""
+    code = textwrap.dedent("""
+        import os, sys
+        sys.path.insert(0, sys.argv[1])
+        import torch.distributed as dist
+        import bench
+        with bench.stdout_to_stderr():
+            dist.init_process_group("gloo")
+            g = dist.new_group(backend="gloo")
+        dist.barrier(group=g)
+        if dist.get_rank() == 0:
+            print('{"line": 1}', flush=True)
+        dist.destroy_process_group()
+    """)
+    plans = bench.rank_plan(2, [], bench.free_port(), base_env=dict(os.environ))
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(ROOT)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for _, env in plans]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
+    assert outs[0][0] == '{"line": 1}\n' and outs[1][0] == ""
