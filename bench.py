@@ -1127,16 +1127,23 @@ def launch_ranks(plans, timeout=None):
     return failed if failed >= 0 else 128 - failed  # killed by signal s -> 128 + s
 
 
-class stdout_to_stderr:
+class StdoutToStderr:
     """File descriptor 1 points at stderr inside the block: native libraries
-    (gloo prints its rendezvous notes with printf) cannot put lines before
-    the one JSON line the driver parses."""
+    (gloo prints its rendezvous notes with printf) and stray prints cannot
+    put lines before the one JSON line the driver parses, which goes to the
+    real stdout through write_line."""
 
     def __enter__(self):
         sys.stdout.flush()
         self.saved = os.dup(1)
         os.dup2(2, 1)
         return self
+
+    def write_line(self, text):
+        sys.stdout.flush()
+        data = (text + "\n").encode()
+        while data:
+            data = data[os.write(self.saved, data):]
 
     def __exit__(self, *exc):
         sys.stdout.flush()
@@ -1184,6 +1191,10 @@ def main():
             log(f"note: {args.gpus} ranks but {ndev} visible GPU(s): a REHEARSAL, ranks share GPUs over gloo")
             argv += ["--dist-backend", "gloo"]
         sys.exit(launch_ranks(rank_plan(args.gpus, argv, free_port())))
+    # stdout carries the one JSON line and nothing else: whatever the
+    # libraries write to file descriptor 1 from here on (gloo's rendezvous
+    # notes, runtime messages) goes to stderr, the line to the saved stdout
+    line_out = StdoutToStderr().__enter__()
     import torch
     import torch.distributed as dist
 
@@ -1197,19 +1208,15 @@ def main():
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(local_rank % max(ndev, 1))
     if world > 1:
-        with stdout_to_stderr():  # gloo's "connected to N peer ranks" notes: stdout carries the line only
-            if args.dist_backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-            else:
-                dist.init_process_group("gloo")
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     # a gloo group for the ranks that wait while rank 0 times the host cores:
     # they block in a socket read, where an RCCL barrier's stream wait could
     # poll on the CPUs the baseline is measuring
-    idle_pg = None
-    if world > 1 and args.dist_backend == "nccl":
-        with stdout_to_stderr():
-            idle_pg = dist.new_group(backend="gloo")
+    idle_pg = dist.new_group(backend="gloo") if world > 1 and args.dist_backend == "nccl" else None
     pg_world = dist.get_world_size() if world > 1 else 1  # the ranks the process group saw
     ident = device_identity(torch.cuda.current_device())
     idents = [ident]
@@ -1427,7 +1434,7 @@ def main():
         if legs:
             out["configs"] = legs
         detail = write_detail(out, args.detail)
-        print(json.dumps(compact_line(out, detail), separators=(",", ":")), flush=True)
+        line_out.write_line(json.dumps(compact_line(out, detail), separators=(",", ":")))
     if world > 1:
         dist.destroy_process_group()
     bad = parity["mismatches"] + (dropin["parity"]["mismatches"] if dropin else 0)

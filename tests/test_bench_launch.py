@@ -479,11 +479,13 @@ def test_stdout_to_stderr_moves_native_writes(capfd):
     """Writes to file descriptor 1 inside the block (as gloo's printf) land
     on stderr; stdout keeps only what is written outside it."""
     print("before", flush=True)
-    with bench.stdout_to_stderr():
+    with bench.StdoutToStderr() as line_out:
         os.write(1, b"native note\n")
+        line_out.write_line('{"line": 1}')
     print("after", flush=True)
     out, err = capfd.readouterr()
-    assert out == "before\nafter\n" and "native note" in err
+    assert out == 'before\n{"line": 1}\nafter\n'
+    assert "native note" in err
 
 
 def test_gloo_group_notes_stay_off_stdout():
@@ -494,12 +496,13 @@ def test_gloo_group_notes_stay_off_stdout():
         sys.path.insert(0, sys.argv[1])
         import torch.distributed as dist
         import bench
-        with bench.stdout_to_stderr():
-            dist.init_process_group("gloo")
-            g = dist.new_group(backend="gloo")
+        out = bench.StdoutToStderr().__enter__()
+        dist.init_process_group("gloo")
+        g = dist.new_group(backend="gloo")
         dist.barrier(group=g)
+        print("stray", flush=True)
         if dist.get_rank() == 0:
-            print('{"line": 1}', flush=True)
+            out.write_line('{"line": 1}')
         dist.destroy_process_group()
     """)
     plans = bench.rank_plan(2, [], bench.free_port(), base_env=dict(os.environ))
@@ -508,3 +511,4 @@ def test_gloo_group_notes_stay_off_stdout():
     outs = [p.communicate(timeout=120) for p in procs]
     assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
     assert outs[0][0] == '{"line": 1}\n' and outs[1][0] == ""
+    assert "stray" in outs[0][1] and "stray" in outs[1][1]
