@@ -184,6 +184,39 @@ __global__ void burst_streams(MixArgs a) {
     }
 }
 
+// The 2-input fp32 sum in place as the library computes it (an add per
+// element, the unordered-compare screen the library's NaN rule runs), but
+// with buffer loads (nt) instead of the library's global nt loads, and the
+// store flavour STORE_AUX: the load form is the one difference from
+// reduce2_kernel<float> (tools/r2_load_ab.py A/Bs the two over placements).
+template <int STORE_AUX>
+__global__ __launch_bounds__(64) void sum2_buffer(const void* in, void* io, uint64_t nvec, uint32_t* sink) {
+    extern __shared__ char lds_cap[];
+    (void)lds_cap;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    if (t0 >= nvec) return;
+    const uint64_t left = nvec - t0;
+    const uint32_t bytes = (uint32_t)(left < 64 ? left : 64) * 16u;
+    const uint32_t off = threadIdx.x * 16u;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(io) + t0 * 16, (short)0,
+                                                                        (int)bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(static_cast<const char*>(in)) + t0 * 16, (short)0, (int)bytes, 0x00020000);
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, kAuxNT);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, kAuxNT);
+    u32x4 r;
+    bool nan = false;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const float x = __uint_as_float(a[e]), y = __uint_as_float(b[e]);
+        const float z = x + y;
+        nan = nan || (z != z);
+        r[e] = __float_as_uint(z);
+    }
+    if (nan) sink[threadIdx.x] = 1u;  // the library refolds such a row; the A/B's inputs hold no NaN
+    __builtin_amdgcn_raw_buffer_store_b128(r, ra, off, 0, STORE_AUX);
+}
+
 typedef hipError_t (*MixFn)(dim3, dim3, unsigned, hipStream_t, const MixArgs&);
 
 template <int K, int T, bool LDS, int AUX>
@@ -336,6 +369,26 @@ __attribute__((visibility("default"))) int mic_mixed_streams(const void* const* 
     if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
     return (int)fn(dim3((unsigned)blocks), dim3((unsigned)block), lds_for(block, waves_per_cu),
                    static_cast<hipStream_t>(stream), a);
+}
+
+// sum2_buffer (see above): io += in over `bytes` of fp32, one-wave
+// workgroups capped at `waves_per_cu` (0 = no cap); flavor 1 = nt stores,
+// 2 = sc1 nt (the library's).  `sink`: 64 uint32 of device memory.
+__attribute__((visibility("default"))) int mic_sum2_buffer(const void* in, void* io, size_t bytes, int waves_per_cu,
+                                                           int flavor, void* sink, void* stream) {
+    if (!in || !io || !sink || bytes % 16 || (flavor != 1 && flavor != 2)) return -1;
+    const uint64_t nvec = bytes / 16;
+    const uint64_t blocks = (nvec + 63) / 64;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return -1;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned lds = lds_for(64, waves_per_cu);
+    if (flavor == 1)
+        hipLaunchKernelGGL(sum2_buffer<kAuxNT>, dim3((unsigned)blocks), dim3(64), lds, s, in, io, nvec,
+                           static_cast<uint32_t*>(sink));
+    else
+        hipLaunchKernelGGL(sum2_buffer<kAuxSC1NT>, dim3((unsigned)blocks), dim3(64), lds, s, in, io, nvec,
+                           static_cast<uint32_t*>(sink));
+    return (int)hipGetLastError();
 }
 
 // burst_streams (see above): K reads and one write, each workgroup of
