@@ -703,36 +703,42 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
         if (threadIdx.x < a.tail) reduce2_elem<Tag, OP, V>(a, a.head + a.nvec * N + threadIdx.x);
     }
     const size_t hb = (size_t)a.head * sizeof(S);
-    const u32x4* p0 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.acc) + hb);
-    const u32x4* p1 = reinterpret_cast<const u32x4*>(static_cast<const char*>(a.in) + hb);
-    // the output through a buffer descriptor: stores with sc1 + nt drop each
-    // line from L2 as it is written; nt alone keeps it there, and the 2-input
-    // stream then ran 2.3-3.1 % slower (tools/occupancy_sweep.hip policy,
+    // Every operand through a buffer descriptor per tile (base = the tile's
+    // first vector, range = its valid bytes; lanes past the end read zeros
+    // and their stores are dropped).  Loads nt: against the global nt loads
+    // of rounds 1-5 the same launch ran 0.3-0.5 % faster at the median and in
+    // each of 16 fresh placements per layout (tools/r2_load_ab.py,
+    // profiles/round6_run6/).  Stores sc1 + nt drop each line from L2 as it
+    // is written; nt alone keeps it there, and the 2-input stream then ran
+    // 2.3-3.1 % slower (tools/occupancy_sweep.hip policy,
     // profiles/round3_occupancy/).  The fan-in keeps nt (sc1 did not pay there).
     const uint64_t t0 = (uint64_t)blk * (B * U);
     const uint64_t tleft = a.nvec > t0 ? a.nvec - t0 : 0;
     const uint32_t tbytes = (uint32_t)(tleft < (uint64_t)B * U ? tleft : (uint64_t)B * U) * 16u;
-    const __amdgpu_buffer_rsrc_t orsrc = tile_rsrc(a.out, hb + t0 * 16, tbytes);
+    const uint64_t tb = hb + t0 * 16;
+    const __amdgpu_buffer_rsrc_t arsrc = tile_rsrc(a.acc, tb, tbytes);
+    const __amdgpu_buffer_rsrc_t irsrc = tile_rsrc(a.in, tb, tbytes);
+    const __amdgpu_buffer_rsrc_t orsrc = tile_rsrc(a.out, tb, tbytes);
     const uint64_t v0 = t0 + threadIdx.x;
     u32x4 x[U], y[U];
-    const bool full = v0 + (uint64_t)(U - 1) * B < a.nvec;
 #pragma unroll
     for (int j = 0; j < U; j++)
-        if (full || v0 + (uint64_t)j * B < a.nvec) x[j] = vload<3>(p0 + v0 + (uint64_t)j * B);
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (uint32_t)(j * B + threadIdx.x) * 16u, 0, kAuxNT);
 #pragma unroll
     for (int j = 0; j < U; j++)
-        if (full || v0 + (uint64_t)j * B < a.nvec) y[j] = vload<3>(p1 + v0 + (uint64_t)j * B);
+        y[j] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, (uint32_t)(j * B + threadIdx.x) * 16u, 0, kAuxNT);
 #pragma unroll
     for (int j = 0; j < U; j++) {
         const uint64_t v = v0 + (uint64_t)j * B;
-        if (full || v < a.nvec) {
+        if (v < a.nvec) {
+            const uint32_t off = (uint32_t)(v - t0) * 16u;
             const u32x4 xs[2] = {x[j], y[j]};
             __builtin_amdgcn_raw_buffer_store_b128(
                 fold_row<Tag, OP, V, 2>(xs, 2, a.head + v * N, a.trunc_from, [&](u32x4 (&r)[2]) {
-                    r[0] = vload<3>(p0 + v);
-                    r[1] = vload<3>(p1 + v);
+                    r[0] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, off, 0, kAuxNT);
+                    r[1] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, off, 0, kAuxNT);
                 }),
-                orsrc, (uint32_t)(v - t0) * 16u, 0, kAuxSC1NT);
+                orsrc, off, 0, kAuxSC1NT);
         }
     }
 }

@@ -29,6 +29,9 @@ def main():
     p.add_argument("--config", default="c2")
     p.add_argument("--rounds", type=int, default=8)
     p.add_argument("--launches", type=int, default=20)
+    p.add_argument("--trials", type=int, default=1,
+                   help="fresh operands (after a random pad) per trial: the A/B over placements")
+    p.add_argument("--layout", default="separate", choices=["separate", "padded", "one"])
     a = p.parse_args()
     import torch
 
@@ -43,12 +46,41 @@ def main():
         L.mi_reduce_multi.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_void_p]
         libs[name] = L
-    ins = [torch.empty(n, dtype=bench.torch_dtype(dt), device="cuda") for _ in range(k)]
+    import random
+    rng = random.Random(17)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    res = {"A": [], "B": []}
+    ratios = []
+    for trial in range(a.trials):
+        torch.cuda.empty_cache()
+        pad_mib = 2 * rng.randrange(0, 1536) if a.trials > 1 else 0
+        pad = torch.empty(pad_mib << 18, dtype=torch.float32, device="cuda") if pad_mib else None
+        ins = bench.alloc_inputs(k, n, bench.torch_dtype(dt), a.layout)
+        tr = one_trial(a, libs, ins, k, n, dt, op, flags, sh, stream, trial)
+        for name in ("A", "B"):
+            res[name] += tr[name]
+        ratios.append(statistics.mean(tr["B"]) / statistics.mean(tr["A"]))
+        del ins, pad
+    algo = (k + 1) * n * es
+    out = {"config": a.config, "layout": a.layout, "trials": a.trials, "lib_a": a.lib_a, "lib_b": a.lib_b,
+           "launches_per_round": a.launches}
+    for name in ("A", "B"):
+        out[name] = {"mean_ms": round(statistics.mean(res[name]), 5), "min_ms": round(min(res[name]), 5),
+                     "frac_of_8TBps_at_mean": round(algo / (statistics.mean(res[name]) / 1e3) / 8e12, 4)}
+    out["B_over_A_mean_time"] = round(statistics.mean(res["B"]) / statistics.mean(res["A"]), 4)
+    out["B_over_A_per_trial"] = {"median": round(statistics.median(ratios), 4), "min": round(min(ratios), 4),
+                                 "max": round(max(ratios), 4)}
+    print(json.dumps(out), flush=True)
+
+
+def one_trial(a, libs, ins, k, n, dt, op, flags, sh, stream, trial):
+    import torch
+
+    import bench
     for j, t in enumerate(ins):
         bench.fill(t, 0xAB + j)
     arr = (ctypes.c_void_p * k)(*[t.data_ptr() for t in ins])
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
 
     def launch(L):
         if k == 2:
@@ -71,14 +103,8 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.launches
             res[name].append(ms)
-            print(json.dumps({"round": r, "lib": name, "avg_launch_ms": round(ms, 5)}), flush=True)
-    algo = (k + 1) * n * es
-    out = {"config": a.config, "lib_a": a.lib_a, "lib_b": a.lib_b, "launches_per_round": a.launches}
-    for name in ("A", "B"):
-        out[name] = {"mean_ms": round(statistics.mean(res[name]), 5), "min_ms": round(min(res[name]), 5),
-                     "frac_of_8TBps_at_mean": round(algo / (statistics.mean(res[name]) / 1e3) / 8e12, 4)}
-    out["B_over_A_mean_time"] = round(statistics.mean(res["B"]) / statistics.mean(res["A"]), 4)
-    print(json.dumps(out), flush=True)
+            print(json.dumps({"trial": trial, "round": r, "lib": name, "avg_launch_ms": round(ms, 5)}), flush=True)
+    return res
 
 
 if __name__ == "__main__":
