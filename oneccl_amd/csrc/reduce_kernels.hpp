@@ -706,9 +706,11 @@ __device__ __forceinline__ void reduce2_tile(const R2Args& a, uint32_t blk) {
     // Every operand through a buffer descriptor per tile (base = the tile's
     // first vector, range = its valid bytes; lanes past the end read zeros
     // and their stores are dropped).  Loads nt: against the global nt loads
-    // of rounds 1-5 the same launch ran 0.3-0.5 % faster at the median and in
-    // each of 16 fresh placements per layout (tools/r2_load_ab.py,
-    // profiles/round6_run6/).  Stores sc1 + nt drop each line from L2 as it
+    // of rounds 1-5 the same fold ran 0.3-0.5 % faster at the median and in
+    // each of 16 fresh placements per layout (tools/r2_load_ab.py), and the
+    // library built this way 0.2-0.5 % faster than the round-5 build over 10
+    // fresh placements per config, C3 bf16 within noise (tools/ab_c2.py
+    // --trials; both in profiles/round6_run6/).  Stores sc1 + nt drop each line from L2 as it
     // is written; nt alone keeps it there, and the 2-input stream then ran
     // 2.3-3.1 % slower (tools/occupancy_sweep.hip policy,
     // profiles/round3_occupancy/).  The fan-in keeps nt (sc1 did not pay there).
