@@ -36,7 +36,8 @@ def main():
     import torch
 
     import bench
-    desc, dt, es, op, k, bucket, flags = bench.CONFIGS[a.config]
+    # "copy": ccl_comp_copy's device kernel (mi_copy), 1 GiB from ins[1] to ins[0]
+    desc, dt, es, op, k, bucket, flags = bench.CONFIGS["c2" if a.config == "copy" else a.config]
     n = bucket // es
     libs = {}
     for name, path in (("A", a.lib_a), ("B", a.lib_b)):
@@ -45,6 +46,7 @@ def main():
                                 ctypes.c_uint, ctypes.c_void_p]
         L.mi_reduce_multi.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_void_p]
+        L.mi_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         libs[name] = L
     import random
     rng = random.Random(17)
@@ -62,7 +64,7 @@ def main():
             res[name] += tr[name]
         ratios.append(statistics.mean(tr["B"]) / statistics.mean(tr["A"]))
         del ins, pad
-    algo = (k + 1) * n * es
+    algo = (2 if a.config == "copy" else k + 1) * n * es
     out = {"config": a.config, "layout": a.layout, "trials": a.trials, "lib_a": a.lib_a, "lib_b": a.lib_b,
            "launches_per_round": a.launches}
     for name in ("A", "B"):
@@ -83,6 +85,8 @@ def one_trial(a, libs, ins, k, n, dt, op, flags, sh, stream, trial):
     arr = (ctypes.c_void_p * k)(*[t.data_ptr() for t in ins])
 
     def launch(L):
+        if a.config == "copy":
+            return L.mi_copy(ins[1].data_ptr(), ins[0].data_ptr(), n * es, 0, sh)
         if k == 2:
             return L.mi_reduce(ins[1].data_ptr(), ins[0].data_ptr(), n, dt, op, flags, sh)
         return L.mi_reduce_multi(arr, k, ins[0].data_ptr(), n, dt, op, flags, sh)
