@@ -59,7 +59,7 @@ def main():
         pad_mib = 2 * rng.randrange(0, 1536) if a.trials > 1 else 0
         pad = torch.empty(pad_mib << 18, dtype=torch.float32, device="cuda") if pad_mib else None
         ins = bench.alloc_inputs(k, n, bench.torch_dtype(dt), a.layout)
-        tr = one_trial(a, libs, ins, k, n, dt, op, flags, sh, stream, trial)
+        tr = one_trial(a, libs, ins, k, n, es, dt, op, flags, sh, stream, trial)
         for name in ("A", "B"):
             res[name] += tr[name]
         ratios.append(statistics.mean(tr["B"]) / statistics.mean(tr["A"]))
@@ -76,7 +76,7 @@ def main():
     print(json.dumps(out), flush=True)
 
 
-def one_trial(a, libs, ins, k, n, dt, op, flags, sh, stream, trial):
+def one_trial(a, libs, ins, k, n, es, dt, op, flags, sh, stream, trial):
     import torch
 
     import bench
