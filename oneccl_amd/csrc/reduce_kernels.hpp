@@ -1164,13 +1164,15 @@ __global__ __launch_bounds__(B) void copy_lean_kernel(const char* __restrict__ s
     const uint64_t t0 = (uint64_t)blockIdx.x * B;
     const uint64_t v = t0 + threadIdx.x;
     if (MEM & 4) {
-        // both sides through per-tile descriptors, nt loads (as reduce2_tile)
+        // global nt loads: buffer loads here ran 0.4-0.7 % slower in every
+        // one of 20 fresh placements (tools/ab_c2.py --config copy,
+        // profiles/round6_run8/), unlike the 2-input reduce's
         const uint64_t tleft = nvec > t0 ? nvec - t0 : 0;
         const uint32_t tbytes = (uint32_t)(tleft < (uint64_t)B ? tleft : (uint64_t)B) * 16u;
-        const __amdgpu_buffer_rsrc_t i = tile_rsrc(src8 + head, t0 * 16, tbytes);
         const __amdgpu_buffer_rsrc_t o = tile_rsrc(dst8 + head, t0 * 16, tbytes);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(i, threadIdx.x * 16u, 0, kAuxNT),
-                                               o, threadIdx.x * 16u, 0, kAuxSC1NT);
+        if (v < nvec)
+            __builtin_amdgcn_raw_buffer_store_b128(vload<MEM & 1>(reinterpret_cast<const u32x4*>(src8 + head) + v), o,
+                                                   threadIdx.x * 16u, 0, kAuxSC1NT);
     } else if (v < nvec) {
         vstore<MEM & 2>(reinterpret_cast<u32x4*>(dst8 + head) + v,
                         vload<MEM & 1>(reinterpret_cast<const u32x4*>(src8 + head) + v));
