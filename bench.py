@@ -331,7 +331,10 @@ class PinnedPool:
         self.errors = []
         self.pin_errors = []  # reported, not raised: an unpinned thread still measures
 
+        self.tids = set()
+
         def body(i, cpu):
+            self.tids.add(threading.get_native_id())
             try:
                 os.sched_setaffinity(0, {cpu})  # pid 0: the calling thread
             except OSError as e:
@@ -365,7 +368,7 @@ class PinnedPool:
             t.join()
 
 
-def cpu_sweep_point(cfg, cpus, seconds, use_ref):
+def cpu_sweep_point(cfg, cpus, seconds, use_ref, pids=None):
     """One thread count of the CPU baseline: len(cpus) threads, each pinned
     to its core, each first-touching its own element range of every buffer
     (so its pages sit on its own NUMA node), then reducing
@@ -421,8 +424,10 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
 
     pool = PinnedPool(cpus)
     pin_errors = pool.pin_errors
+    moved = {}
     try:
         pool.run(touch)
+        moved = clear_cores(set(cpus), pool.tids, pids)
         pool.run(reduce)  # warm
         times = []
         st0, ps0 = cgroup_cpu_stat(), psi_totals()
@@ -433,6 +438,7 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
             times.append(time.perf_counter() - t0)
         st1, ps1 = cgroup_cpu_stat(), psi_totals()
     finally:
+        restore_affinity(moved)
         pool.close()
     del ins, acc
     throttle = {k: st1[k] - st0[k] for k in ("nr_periods", "nr_throttled", "throttled_usec")
@@ -442,6 +448,42 @@ def cpu_sweep_point(cfg, cpus, seconds, use_ref):
     throttle.update({f"psi_{k}_some_us": ps1[k] - ps0[k] for k in ps0 if k in ps1})
     return (bucket / GiB / min(times), bucket / GiB / statistics.median(times), len(times), list(pin_errors),
             throttle)
+
+
+def clear_cores(cores, keep, pids=None):
+    """Move every other thread of this process (the main thread, the HIP
+    runtime's, the library's helpers) and of `pids` (the other ranks of an
+    N-rank run, waiting meanwhile) off `cores` while the timing threads
+    (native ids `keep`) run there, so none of them queues behind another
+    thread on its core.  Returns {tid: previous affinity} for
+    restore_affinity; threads that cannot be moved are left as they are."""
+    moved = {}
+    tids = []
+    for pid in pids or [os.getpid()]:
+        try:
+            tids += [int(t) for t in os.listdir(f"/proc/{pid}/task")]
+        except OSError:
+            continue
+    for tid in tids:
+        if tid in keep:
+            continue
+        try:
+            prev = os.sched_getaffinity(tid)
+            rest = prev - cores
+            if rest and rest != prev:
+                os.sched_setaffinity(tid, rest)
+                moved[tid] = prev
+        except OSError:
+            continue
+    return moved
+
+
+def restore_affinity(moved):
+    for tid, prev in moved.items():
+        try:
+            os.sched_setaffinity(tid, prev)
+        except OSError:
+            pass  # the thread has exited
 
 
 def cgroup_cpu_stat(path="/sys/fs/cgroup/cpu.stat"):
@@ -485,7 +527,7 @@ def sweep_counts(n_cores, quota):
     return counts, [t for t in (8, 16, 32, 64) if t not in counts]
 
 
-def cpu_baseline(cfg, seconds):
+def cpu_baseline(cfg, seconds, pids=None):
     """The reference's own CPU reduce (or, for the bf16/fp16 types it cannot
     reach standalone, the oracle's restatement) timed on this host's cores,
     a bounded sample: 1 thread (one ccl_worker, CCL_WORKER_COUNT=1 default)
@@ -502,10 +544,10 @@ def cpu_baseline(cfg, seconds):
     share = max(seconds / (len(counts) + 1), 1.0)
     res = {}
     for t in counts:
-        res[t] = cpu_sweep_point(cfg, cores[:t] if cores else [0], share * (2 if t == 1 else 1), use_ref)
+        res[t] = cpu_sweep_point(cfg, cores[:t] if cores else [0], share * (2 if t == 1 else 1), use_ref, pids)
     port_1 = None
     if use_ref:  # the restatement on the same bucket, one thread, for comparison
-        port_1 = round(cpu_sweep_point(cfg, cores[:1] if cores else [0], 1.0, False)[0], 3)
+        port_1 = round(cpu_sweep_point(cfg, cores[:1] if cores else [0], 1.0, False, pids)[0], 3)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -566,7 +608,8 @@ def cpu_baseline(cfg, seconds):
                                  "domains (CCDs), pinned; each thread first-touches "
                                  "its own range of every buffer, then reduces it; thread counts above the node's "
                                  "physical cores, or above the cgroup's CPU quota - 1, are skipped; throttle = the "
-                                 "cgroup's cpu.stat deltas over each point's timed reps"},
+                                 "cgroup's cpu.stat deltas over each point's timed reps; the process's other threads (and the other "
+                                 "ranks') are moved off the timing cores while a point runs"},
         "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
     }
 
@@ -1224,6 +1267,10 @@ def main():
         idents = [None] * pg_world
         dist.all_gather_object(idents, ident)
     n_devices, ranks_per_device, rehearsal = device_plan(idents)
+    pids = [os.getpid()]  # every rank's process: rank 0 keeps them off its timing cores (cpu_baseline)
+    if world > 1:
+        pids = [None] * pg_world
+        dist.all_gather_object(pids, os.getpid())
 
     cfg = CONFIGS[args.config]
     desc, dt, es, op, k, bucket, flags = cfg
@@ -1313,7 +1360,7 @@ def main():
         dist.barrier()  # every rank is past its timed region before rank 0 loads the host cores
     if rank == 0 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(cfg, args.cpu_seconds)
+            cpu = cpu_baseline(cfg, args.cpu_seconds, pids)
         except Exception as e:  # noqa: BLE001 - a reported baseline never costs the line
             cpu = {"error": f"{type(e).__name__}: {e}"}
             log(f"cpu_baseline failed: {cpu['error']}")

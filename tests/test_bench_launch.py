@@ -512,3 +512,52 @@ def test_gloo_group_notes_stay_off_stdout():
     assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
     assert outs[0][0] == '{"line": 1}\n' and outs[1][0] == ""
     assert "stray" in outs[0][1] and "stray" in outs[1][1]
+
+
+def test_clear_cores_moves_other_threads_and_restores():
+    """During a sweep point every thread of the process but the timing ones
+    leaves the timing cores, and gets its affinity back afterwards."""
+    import threading
+    aff = sorted(os.sched_getaffinity(0))
+    if len(aff) < 3:
+        pytest.skip("needs 3+ CPUs")
+    stop = threading.Event()
+    seen = {}
+
+    def idle():
+        seen["tid"] = threading.get_native_id()
+        stop.wait(30)
+
+    t = threading.Thread(target=idle)
+    t.start()
+    while "tid" not in seen:
+        pass
+    try:
+        cores = {aff[0]}
+        moved = bench.clear_cores(cores, keep=set())
+        assert seen["tid"] in moved and threading.get_native_id() in moved
+        assert not os.sched_getaffinity(seen["tid"]) & cores
+        assert not os.sched_getaffinity(0) & cores
+        bench.restore_affinity(moved)
+        assert os.sched_getaffinity(seen["tid"]) == set(aff) and os.sched_getaffinity(0) == set(aff)
+    finally:
+        stop.set()
+        t.join()
+
+
+def test_clear_cores_moves_another_process_threads():
+    """An N-rank run's other ranks (their pids) leave the timing cores too."""
+    aff = sorted(os.sched_getaffinity(0))
+    if len(aff) < 3:
+        pytest.skip("needs 3+ CPUs")
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        cores = {aff[-1]}
+        moved = bench.clear_cores(cores, keep=set(), pids=[p.pid])
+        assert p.pid in moved and not os.sched_getaffinity(p.pid) & cores
+        assert os.getpid() not in moved  # only the pids named
+        bench.restore_affinity(moved)
+        assert os.sched_getaffinity(p.pid) == set(aff)
+    finally:
+        p.kill()
+        p.wait()
