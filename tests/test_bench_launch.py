@@ -561,3 +561,17 @@ def test_clear_cores_moves_another_process_threads():
     finally:
         p.kill()
         p.wait()
+
+
+def test_compact_line_keeps_a_failed_cpu_baseline_and_no_legs():
+    """A CPU baseline that failed is carried as its error, and a line without
+    config legs, host leg or strong split (a --no-config-legs run) stays
+    well-formed."""
+    full = _canned_full()
+    full["cpu_baseline"] = {"error": "OSError: no cores"}
+    for k in ("configs", "host_resident", "dropin_sync"):
+        full.pop(k)
+    line = bench.compact_line(full, "profiles/bench_detail.json")
+    assert line["cpu_baseline"] == {"error": "OSError: no cores"}
+    assert "configs" not in line and "host_resident" not in line and "trimmed" not in line
+    assert json.loads(json.dumps(line)) == line
